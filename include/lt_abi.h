@@ -1,0 +1,146 @@
+/*
+ * lt_abi.h — C ABI of the MI355X LandTrendr analysis engine (land_trendr_amd/liblt_hip.so).
+ *
+ * Drop-in boundary for the reference's per-pixel hot path. The reference is pure Python and binds
+ * no native code; this ABI replaces, per batched tile of pixels:
+ *   - utils.analyze(pix_datas, line_cost, target_date)        /root/reference/utils.py:735-789
+ *       pick_winners :491-521, dicts2timeseries :523-532, despike :556-582,
+ *       timeseries2int_series :534-554, least_squares :584-598, segmented_least_squares :600-631,
+ *       find_segments :633-644, vertices2eqns :646-669, eqns2fitted_points :682-722
+ *   - utils.change_labeling(trendline, label_rules)          /root/reference/utils.py:795-820
+ *       Trendline.parse_disturbances / match_rule             /root/reference/classes.py:156-232
+ *   - the per-pixel loop of MRLandTrendrJob.analysis_reducer  /root/reference/mr_land_trendr_job.py:83-126
+ *     (one call per grid point there; one call per pixel tile here).
+ * The Python host (land_trendr_amd/utils.py, classes.py) binds it with ctypes; INTEGRATION.md shows
+ * the binding. Plain C types only: no torch types cross this boundary.
+ *
+ * Memory: the caller owns every buffer. lt_tile_in / lt_tile_out pointers are DEVICE pointers
+ * (hipMalloc or torch tensors on the context's device); lt_scene / lt_params are HOST structs that
+ * the call copies. Any lt_tile_out pointer may be NULL: that field is not written.
+ * Layout: pixel-major structure of arrays. Plane q of a field starts at base + q*stride, the pixel
+ * index runs fastest, so lane i of a wavefront touches element i of a plane (coalesced).
+ */
+#ifndef LT_ABI_H
+#define LT_ABI_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LT_ABI_VERSION 1
+#define LT_MAX_YEARS 64   /* distinct calendar years per scene (T <= 40 in every config) */
+#define LT_MAX_OBS 1024   /* observations per scene (K*T) */
+#define LT_MAX_RULES 16
+#define LT_NODATA (-99)   /* settings.py:16 */
+
+/* Per-pixel status bits (lt_tile_out.status). Non-zero = the reference raises for this pixel. */
+enum {
+  LT_ST_OK = 0,
+  LT_ST_EMPTY = 1,              /* no valid observation: reference IndexError (utils.py:569)     */
+  LT_ST_SINGLE_YEAR = 2,        /* T == 1: reference ValueError in despike (utils.py:582)        */
+  LT_ST_PRE_THRESHOLD_ATTR = 4, /* pre_threshold in reference mode: AttributeError (classes.py:207) */
+  LT_ST_FEB29 = 8,              /* Feb-29 target in a non-leap year: ValueError (utils.py:511)   */
+  LT_ST_NUMERIC = 16            /* LAPACK path not emulated (rank < 2 / DLASCL rescaling)        */
+};
+
+/* Return codes of the API functions. */
+enum {
+  LT_OK = 0,
+  LT_ERR_ARG = -1,
+  LT_ERR_HIP = -2,
+  LT_ERR_JIT = -3,
+  LT_ERR_LIMIT = -4
+};
+
+enum { LT_CT_NONE = 0, LT_CT_FD = 1, LT_CT_GD = 2, LT_CT_LD = 3 };          /* classes.py:44-47 */
+enum { LT_Q_UNSET = 0, LT_Q_EQ = 1, LT_Q_LE = 2, LT_Q_GE = 3, LT_Q_GT = 4, LT_Q_LT = 5,
+       LT_Q_OTHER = 9 /* set, but a qualifier match_rule ignores (classes.py:190-211) */ };
+enum { LT_PRE_REFERENCE = 0, LT_PRE_DOCUMENTED = 1 };                      /* SURVEY App. B #1 */
+
+/* One validated LabelRule (classes.py:32-64). The host performs the validation. */
+typedef struct {
+  int32_t change_type;   /* LT_CT_*                                  */
+  int32_t onset_op;      /* LT_Q_UNSET / EQ / LE / GE / OTHER        */
+  int32_t duration_op;   /* LT_Q_UNSET / GT / LT / OTHER             */
+  int32_t pre_op;        /* LT_Q_UNSET / GT / LT / OTHER             */
+  double onset_val;
+  double duration_val;
+  double pre_val;
+  int32_t class_val;     /* rule.val, written to the class raster    */
+  int32_t _pad;
+} lt_rule;
+
+/* settings.json semantics (README.md:46-85) minus target_date, which is folded into lt_scene. */
+typedef struct {
+  double line_cost;
+  int32_t n_rules;
+  int32_t pre_threshold_mode; /* LT_PRE_* */
+  lt_rule rules[LT_MAX_RULES];
+} lt_params;
+
+/* Observation metadata shared by every pixel of a tile (all pixels of a co-registered stack see
+ * the same acquisition dates). Built on the host from the dates and target_date
+ * (land_trendr_amd/scene.py restates pick_winners' grouping, utils.py:503-517). */
+typedef struct {
+  int32_t n_obs;              /* K                                                          */
+  int32_t n_years;            /* Y distinct calendar years, ascending                       */
+  const int32_t* year;        /* [Y]   calendar year of slot y                              */
+  const int32_t* slot_begin;  /* [Y+1] slot y covers order[slot_begin[y] .. slot_begin[y+1]) */
+  const int32_t* order;       /* [K]   obs ids grouped by slot, caller's input order inside  */
+  const int32_t* dist;        /* [K]   abs((target(year) - date).days) for order[k]          */
+  const uint8_t* feb29_bad;   /* [Y]   1: target is Feb-29 and year y is not a leap year     */
+} lt_scene;
+
+typedef struct {
+  int64_t n_pix;              /* P                                                          */
+  int64_t stride;             /* elements between obs planes (>= n_pix)                     */
+  const double* obs_val;      /* [K][stride] observation values (float(val), utils.py:357)  */
+  const uint8_t* obs_valid;   /* [K][stride] 0 = cloud-masked (utils.py:353); NULL = all    */
+} lt_tile_in;
+
+typedef struct {
+  int64_t stride;             /* elements between year / rule planes (>= n_pix)             */
+  int32_t* status;            /* [P]    LT_ST_* bits                                        */
+  int32_t* n_years;           /* [P]    T: years present for the pixel                      */
+  int16_t* winner;            /* [Y][stride] winning obs id, -1 = year absent for the pixel */
+  double* val_raw;            /* [Y][stride] TrendlinePoint fields (classes.py:67-116);     */
+  double* val_fit;            /*             absent years are written NaN / 0               */
+  double* fit_m;
+  double* fit_b;
+  double* right_m;
+  double* right_b;
+  uint8_t* spike;
+  uint8_t* vertex;
+  uint8_t* matched;           /* [R][stride] change_labeling (utils.py:795-820)             */
+  int32_t* class_val;         /*             rule.val if matched else LT_NODATA             */
+  int32_t* onset_year;        /*             LT_NODATA if unmatched                         */
+  int32_t* duration;
+  double* magnitude;          /*             LT_NODATA if unmatched                         */
+  double* initial_val;
+} lt_tile_out;
+
+typedef struct lt_ctx lt_ctx;
+
+int lt_abi_version(void);
+/* Bind a context to a HIP device. Not thread-safe: one context per thread / GPU. */
+int lt_ctx_create(int device, lt_ctx** out);
+int lt_ctx_destroy(lt_ctx* ctx);
+const char* lt_last_error(const lt_ctx* ctx);
+
+/* Full analyze + label of one tile, asynchronous on `stream` (a hipStream_t; NULL = default).
+ * Kernels: winner selection (pick_winners) then the fused despike / segmented-least-squares /
+ * fit / label kernel. */
+int lt_analyze_tile(lt_ctx* ctx, const lt_scene* scene, const lt_params* params,
+                    const lt_tile_in* in, const lt_tile_out* out, void* stream);
+
+/* Stage timing: when enabled, each lt_analyze_tile brackets its kernels with hipEvents on the
+ * launch stream; lt_ctx_stage_ms returns the accumulated milliseconds per stage
+ * (0 = winner selection, 1 = analyze/label) since the last reset and the launch count. */
+int lt_ctx_set_timing(lt_ctx* ctx, int enable);
+int lt_ctx_stage_ms(lt_ctx* ctx, double* ms_out, int n_stages, int64_t* n_launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

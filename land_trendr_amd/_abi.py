@@ -1,0 +1,104 @@
+"""ctypes mirror of include/lt_abi.h and the loader of the HIP library.
+
+The library is built in-tree by __graft_entry__.build() (hipcc --offload-arch=gfx950) into
+land_trendr_amd/liblt_hip.so. There is no CPU fallback: if the library is missing, load_lib()
+raises, so a GPU run can never silently pass on something other than the HIP kernels.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, 'liblt_hip.so')
+
+LT_ABI_VERSION = 1
+LT_MAX_YEARS = 64
+LT_MAX_OBS = 1024
+LT_MAX_RULES = 16
+LT_NODATA = -99
+
+LT_ST_OK, LT_ST_EMPTY, LT_ST_SINGLE_YEAR = 0, 1, 2
+LT_ST_PRE_THRESHOLD_ATTR, LT_ST_FEB29, LT_ST_NUMERIC = 4, 8, 16
+
+LT_CT = {None: 0, 'FD': 1, 'GD': 2, 'LD': 3}
+LT_Q_UNSET, LT_Q_EQ, LT_Q_LE, LT_Q_GE, LT_Q_GT, LT_Q_LT, LT_Q_OTHER = 0, 1, 2, 3, 4, 5, 9
+LT_PRE_REFERENCE, LT_PRE_DOCUMENTED = 0, 1
+
+c_i32p = ctypes.POINTER(ctypes.c_int32)
+c_i16p = ctypes.POINTER(ctypes.c_int16)
+c_u8p = ctypes.POINTER(ctypes.c_uint8)
+c_f64p = ctypes.POINTER(ctypes.c_double)
+
+
+class LtRule(ctypes.Structure):
+    _fields_ = [('change_type', ctypes.c_int32), ('onset_op', ctypes.c_int32),
+                ('duration_op', ctypes.c_int32), ('pre_op', ctypes.c_int32),
+                ('onset_val', ctypes.c_double), ('duration_val', ctypes.c_double),
+                ('pre_val', ctypes.c_double), ('class_val', ctypes.c_int32),
+                ('_pad', ctypes.c_int32)]
+
+
+class LtParams(ctypes.Structure):
+    _fields_ = [('line_cost', ctypes.c_double), ('n_rules', ctypes.c_int32),
+                ('pre_threshold_mode', ctypes.c_int32), ('rules', LtRule * LT_MAX_RULES)]
+
+
+class LtScene(ctypes.Structure):
+    _fields_ = [('n_obs', ctypes.c_int32), ('n_years', ctypes.c_int32), ('year', c_i32p),
+                ('slot_begin', c_i32p), ('order', c_i32p), ('dist', c_i32p),
+                ('feb29_bad', c_u8p)]
+
+
+class LtTileIn(ctypes.Structure):
+    _fields_ = [('n_pix', ctypes.c_int64), ('stride', ctypes.c_int64), ('obs_val', c_f64p),
+                ('obs_valid', c_u8p)]
+
+
+class LtTileOut(ctypes.Structure):
+    _fields_ = [('stride', ctypes.c_int64), ('status', c_i32p), ('n_years', c_i32p),
+                ('winner', c_i16p), ('val_raw', c_f64p), ('val_fit', c_f64p), ('fit_m', c_f64p),
+                ('fit_b', c_f64p), ('right_m', c_f64p), ('right_b', c_f64p), ('spike', c_u8p),
+                ('vertex', c_u8p), ('matched', c_u8p), ('class_val', c_i32p),
+                ('onset_year', c_i32p), ('duration', c_i32p), ('magnitude', c_f64p),
+                ('initial_val', c_f64p)]
+
+
+# per-year outputs [Y][stride] and per-rule outputs [R][stride]: (field, numpy dtype)
+YEAR_FIELDS = [('winner', 'int16'), ('val_raw', 'float64'), ('val_fit', 'float64'),
+               ('fit_m', 'float64'), ('fit_b', 'float64'), ('right_m', 'float64'),
+               ('right_b', 'float64'), ('spike', 'uint8'), ('vertex', 'uint8')]
+RULE_FIELDS = [('matched', 'uint8'), ('class_val', 'int32'), ('onset_year', 'int32'),
+               ('duration', 'int32'), ('magnitude', 'float64'), ('initial_val', 'float64')]
+PIX_FIELDS = [('status', 'int32'), ('n_years', 'int32')]
+
+# symbols include/lt_abi.h declares (checked by tests/test_abi.py)
+EXPORTS = ['lt_abi_version', 'lt_ctx_create', 'lt_ctx_destroy', 'lt_last_error',
+           'lt_analyze_tile', 'lt_ctx_set_timing', 'lt_ctx_stage_ms']
+
+_LIB = None
+
+
+def load_lib(path=None):
+    """Load liblt_hip.so and declare its signatures. Raises if the HIP library is absent."""
+    global _LIB
+    if _LIB is not None and path is None:
+        return _LIB
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise RuntimeError('HIP library %s not built: run __graft_entry__.build() '
+                           '(no CPU fallback exists)' % p)
+    lib = ctypes.CDLL(p)
+    vp = ctypes.c_void_p
+    lib.lt_abi_version.restype = ctypes.c_int
+    lib.lt_ctx_create.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
+    lib.lt_ctx_destroy.argtypes = [vp]
+    lib.lt_last_error.argtypes = [vp]
+    lib.lt_last_error.restype = ctypes.c_char_p
+    lib.lt_analyze_tile.argtypes = [vp, ctypes.POINTER(LtScene), ctypes.POINTER(LtParams),
+                                    ctypes.POINTER(LtTileIn), ctypes.POINTER(LtTileOut), vp]
+    lib.lt_ctx_set_timing.argtypes = [vp, ctypes.c_int]
+    lib.lt_ctx_stage_ms.argtypes = [vp, c_f64p, ctypes.c_int, ctypes.POINTER(ctypes.c_int64)]
+    if lib.lt_abi_version() != LT_ABI_VERSION:
+        raise RuntimeError('liblt_hip.so ABI %d != %d' % (lib.lt_abi_version(), LT_ABI_VERSION))
+    if path is None:
+        _LIB = lib
+    return lib

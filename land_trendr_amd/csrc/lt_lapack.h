@@ -1,0 +1,488 @@
+// lt_lapack.h — np.linalg.lstsq([x | 1], y) for one segment, bit-for-bit as the reference reaches
+// it (utils.py:594-597 → numpy 2.2.6 → OpenBLAS 0.3.29 SkylakeX dgelsd), restated for CDNA4.
+//
+// Arithmetic recipe: SURVEY.md Appendix A. Differences from a textbook Householder solve, all of
+// which decide DP tie-breaks on integer Landsat data:
+//   * dnrm2 is x87 code (80-bit accumulators, 64-bit significand): emulated here in integer
+//     arithmetic (f80_* below) — the x87 unit has no counterpart on the GPU;
+//   * dgemv_t sums in four interleaved lanes plus an FMA tail; daxpy/drot fuse (explicit fma());
+//   * everything else is separately rounded binary64 (build with -ffp-contract=off).
+// The segment vectors (the ones column after H1, b after H1/H2) are never materialised: every
+// pass recomputes element k from x[k], y[k] and the pass-invariant scalars, so one lane carries a
+// whole segment in ~20 registers. Functions are __host__ __device__ so the tests can run this exact
+// code on the CPU against the oracle (tests/native/lapack_host_check.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace lt {
+
+// ------------------------------------------------------------------------------------------------
+// Non-negative soft float80: value = sig * 2^(exp - 63), sig normalised (bit 63 set) or 0.
+// Only squares of doubles, sums of non-negatives and one final sqrt are ever needed (dnrm2).
+// ------------------------------------------------------------------------------------------------
+struct f80 {
+  uint64_t sig;
+  int32_t exp;
+};
+
+__host__ __device__ inline uint64_t dbl_bits(double d) { return __builtin_bit_cast(uint64_t, d); }
+
+// x87 fmul of a double by itself: exact 106-bit product rounded to a 64-bit significand (RNE).
+__host__ __device__ inline f80 f80_sq(double d) {
+  uint64_t b = dbl_bits(d) & 0x7fffffffffffffffull;
+  if (b == 0) return f80{0, 0};
+  int32_t e = (int32_t)(b >> 52);
+  uint64_t m = b & 0x000fffffffffffffull;
+  if (e == 0) {  // subnormal: normalise
+    int sh = __builtin_clzll(m) - 11;
+    m <<= sh;
+    e = 1 - sh;
+  } else {
+    m |= 0x0010000000000000ull;
+  }
+  unsigned __int128 P = (unsigned __int128)m * m;  // in [2^104, 2^106)
+  int sh = ((uint64_t)(P >> 64) >> 41) ? 42 : 41;
+  uint64_t sig = (uint64_t)(P >> sh);
+  uint64_t rem = (uint64_t)P & ((1ull << sh) - 1);
+  uint64_t half = 1ull << (sh - 1);
+  int32_t ex = sh + 2 * e - 2087;
+  if (rem > half || (rem == half && (sig & 1))) {
+    sig++;
+    if (sig == 0) {
+      sig = 1ull << 63;
+      ex++;
+    }
+  }
+  return f80{sig, ex};
+}
+
+// x87 fadd of two non-negative extended values, RNE to a 64-bit significand.
+__host__ __device__ inline f80 f80_add(f80 a, f80 b) {
+  if (b.sig == 0) return a;
+  if (a.sig == 0) return b;
+  if (a.exp < b.exp) {
+    f80 t = a;
+    a = b;
+    b = t;
+  }
+  int32_t d = a.exp - b.exp;
+  if (d > 64) return a;  // b < half an ulp of a
+  uint64_t bhi, blo;
+  if (d == 0) {
+    bhi = b.sig;
+    blo = 0;
+  } else if (d < 64) {
+    bhi = b.sig >> d;
+    blo = b.sig << (64 - d);
+  } else {
+    bhi = 0;
+    blo = b.sig;
+  }
+  uint64_t hi = a.sig + bhi;
+  uint64_t sig, rbit, sticky;
+  int32_t ex = a.exp;
+  if (hi < a.sig) {  // carry out: 65-bit sum
+    sig = (1ull << 63) | (hi >> 1);
+    rbit = hi & 1;
+    sticky = blo != 0;
+    ex++;
+  } else {
+    sig = hi;
+    rbit = blo >> 63;
+    sticky = (blo << 1) != 0;
+  }
+  if (rbit && (sticky || (sig & 1))) {
+    sig++;
+    if (sig == 0) {
+      sig = 1ull << 63;
+      ex++;
+    }
+  }
+  return f80{sig, ex};
+}
+
+// (double) sqrtl(t): square root rounded to 64 bits (RNE), then to 53 bits (RNE) — the double
+// rounding of x87 fsqrt followed by fstpl.
+__host__ __device__ inline double f80_sqrt_to_double(f80 t) {
+  if (t.sig == 0) return 0.0;
+  int32_t ep = t.exp - 63;           // t = sig * 2^ep
+  int s = ((ep - 63) & 1) ? 64 : 63;  // ep - s even
+  unsigned __int128 N = (unsigned __int128)t.sig << s;  // in [2^126, 2^128)
+  int32_t half_e = (ep - s) / 2;      // exact (even)
+  // integer square root: floating estimate, one Newton correction, exact fix-up
+  double Nd = (double)(uint64_t)(N >> 64) * 0x1p64 + (double)(uint64_t)N;
+  double qd = __builtin_sqrt(Nd);
+  uint64_t q = qd >= 0x1p64 ? ~0ull : (uint64_t)qd;
+  {
+    unsigned __int128 q2 = (unsigned __int128)q * q;
+    double diff = q2 > N ? -(double)(q2 - N) : (double)(N - q2);
+    double dq = diff / (2.0 * (double)q);
+    int64_t step = (int64_t)(dq >= 0 ? dq + 0.5 : dq - 0.5);
+    q = (uint64_t)((int64_t)q + step);
+  }
+  while ((unsigned __int128)q * q > N) q--;
+  while (q != ~0ull && (unsigned __int128)(q + 1) * (q + 1) <= N) q++;
+  unsigned __int128 rem = N - (unsigned __int128)q * q;
+  int32_t ex = half_e;
+  if (rem > (unsigned __int128)q) {  // sqrt(N) > q + 1/2 (never exactly)
+    if (q == ~0ull) {
+      q = 1ull << 63;
+      ex++;
+    } else {
+      q++;
+    }
+  }
+  // round the 64-bit significand to 53 bits
+  uint64_t mant = q >> 11;
+  uint64_t r = q & 0x7ff;
+  if (r > 0x400 || (r == 0x400 && (mant & 1))) {
+    mant++;
+    if (mant == (1ull << 53)) {
+      mant = 1ull << 52;
+      ex++;
+    }
+  }
+  return __builtin_ldexp((double)mant, ex + 11);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Streaming BLAS pieces. Element k of the vector is produced by a callable `get(k)`.
+// ------------------------------------------------------------------------------------------------
+
+// OpenBLAS dnrm2_k SkylakeX over n elements: 4 x87 accumulators in 8-element blocks.
+template <class G>
+__host__ __device__ inline double nrm2(int n, G get) {
+  if (n <= 0) return 0.0;
+  if (n == 1) return __builtin_fabs(get(0));
+  f80 a0{0, 0}, a1{0, 0}, a2{0, 0}, a3{0, 0};
+  int n8 = n & ~7, j = 0;
+  for (; j < n8; j += 4) {
+    a0 = f80_add(a0, f80_sq(get(j)));
+    a1 = f80_add(a1, f80_sq(get(j + 1)));
+    a2 = f80_add(a2, f80_sq(get(j + 2)));
+    a3 = f80_add(a3, f80_sq(get(j + 3)));
+  }
+  for (; j < n; j++) a0 = f80_add(a0, f80_sq(get(j)));
+  f80 t = f80_add(f80_add(f80_add(a0, a2), a1), a3);
+  return f80_sqrt_to_double(t);
+}
+
+// OpenBLAS dgemv_t SkylakeX, one column: sum_k a(k) v(k) with 4 interleaved lanes + FMA tail.
+template <class GA, class GV>
+__host__ __device__ inline double gemv_t1(int m, GA a, GV v) {
+  int m3 = m & 3, m1 = m - m3;
+  double y = 0.0;
+  if (m1 > 0) {
+    double L0 = 0.0, L1 = 0.0, L2 = 0.0, L3 = 0.0;
+    for (int i = 0; i < m1; i += 4) {
+      L0 = L0 + a(i) * v(i);
+      L1 = L1 + a(i + 1) * v(i + 1);
+      L2 = L2 + a(i + 2) * v(i + 2);
+      L3 = L3 + a(i + 3) * v(i + 3);
+    }
+    double r = (L0 + L2) + (L1 + L3);
+    y = __builtin_fma(r, 1.0, y);
+  }
+  if (m3 == 1) {
+    y = __builtin_fma(a(m1), v(m1), y);
+  } else if (m3 == 2) {
+    y = y + __builtin_fma(a(m1), v(m1), a(m1 + 1) * v(m1 + 1));
+  } else if (m3 == 3) {
+    y = y + __builtin_fma(a(m1 + 2), v(m1 + 2), __builtin_fma(a(m1), v(m1), a(m1 + 1) * v(m1 + 1)));
+  }
+  return y;
+}
+
+__host__ __device__ inline double dlapy2(double x, double y) {
+  double xa = __builtin_fabs(x), ya = __builtin_fabs(y);
+  double w = xa > ya ? xa : ya;
+  double z = xa < ya ? xa : ya;
+  if (z == 0.0) return w;
+  double t = z / w;
+  return w * __builtin_sqrt(1.0 + t * t);
+}
+
+__host__ __device__ inline double fsign(double a, double b) {
+  return __builtin_copysign(__builtin_fabs(a), b);
+}
+
+// DLASV2 (LAPACK 3.x), literal transcription.
+__host__ __device__ inline void dlasv2(double f, double g, double h, double& ssmin, double& ssmax,
+                                       double& snr, double& csr, double& snl, double& csl) {
+  const double eps = 0x1p-53;
+  double ft = f, fa = __builtin_fabs(ft), ht = h, ha = __builtin_fabs(h);
+  int pmax = 1;
+  bool swap = ha > fa;
+  if (swap) {
+    pmax = 3;
+    double tmp = ft;
+    ft = ht;
+    ht = tmp;
+    tmp = fa;
+    fa = ha;
+    ha = tmp;
+  }
+  double gt = g, ga = __builtin_fabs(gt);
+  double clt, crt, slt, srt, smin, smax;
+  if (ga == 0.0) {
+    smin = ha;
+    smax = fa;
+    clt = 1.0;
+    crt = 1.0;
+    slt = 0.0;
+    srt = 0.0;
+  } else {
+    bool gasmal = true;
+    if (ga > fa) {
+      pmax = 2;
+      if ((fa / ga) < eps) {
+        gasmal = false;
+        smax = ga;
+        smin = (ha > 1.0) ? fa / (ga / ha) : (fa / ga) * ha;
+        clt = 1.0;
+        slt = ht / gt;
+        srt = 1.0;
+        crt = ft / gt;
+      }
+    }
+    if (gasmal) {
+      double d = fa - ha;
+      double l = (d == fa) ? 1.0 : d / fa;
+      double m = gt / ft;
+      double t = 2.0 - l;
+      double mm = m * m, tt = t * t;
+      double s = __builtin_sqrt(tt + mm);
+      double r = (l == 0.0) ? __builtin_fabs(m) : __builtin_sqrt(l * l + mm);
+      double a = 0.5 * (s + r);
+      smin = ha / a;
+      smax = fa * a;
+      if (mm == 0.0) {
+        if (l == 0.0) t = fsign(2.0, ft) * fsign(1.0, gt);
+        else t = gt / fsign(d, ft) + m / t;
+      } else {
+        t = (m / (s + t) + m / (r + l)) * (1.0 + a);
+      }
+      l = __builtin_sqrt(t * t + 4.0);
+      crt = 2.0 / l;
+      srt = t / l;
+      clt = (crt + srt * m) / a;
+      slt = ((ht / ft) * srt) / a;
+    }
+  }
+  if (swap) {
+    csl = srt; snl = crt; csr = slt; snr = clt;
+  } else {
+    csl = clt; snl = slt; csr = crt; snr = srt;
+  }
+  double tsign;
+  if (pmax == 1) tsign = fsign(1.0, csr) * fsign(1.0, csl) * fsign(1.0, f);
+  else if (pmax == 2) tsign = fsign(1.0, snr) * fsign(1.0, csl) * fsign(1.0, g);
+  else tsign = fsign(1.0, snr) * fsign(1.0, snl) * fsign(1.0, h);
+  ssmax = fsign(smax, tsign);
+  ssmin = fsign(smin, tsign * fsign(1.0, f) * fsign(1.0, h));
+}
+
+// DLALSD, N = 2: DLASDQ/DBDSQR on the 2x2 upper bidiagonal (d1, e; d2), solve, back-transform.
+// Returns the numerical rank, or -1 for the DLASCL rescaling path (not emulated).
+__host__ __device__ inline int dlalsd2(double d1, double d2, double e, double b1, double b2,
+                                       double rcond, double& x0, double& x1) {
+  const double eps = 0x1p-53, unfl = 0x1p-1022;
+  const double tolmul = 98.70149282610821;  // max(10, min(100, eps^(-1/8)))
+  double rcnd = (rcond > 0.0 && rcond < 1.0) ? rcond : eps;
+  double org = __builtin_fabs(d1);
+  if (__builtin_fabs(d2) > org) org = __builtin_fabs(d2);
+  if (__builtin_fabs(e) > org) org = __builtin_fabs(e);
+  if (org == 0.0) {
+    x0 = 0.0;
+    x1 = 0.0;
+    return 0;
+  }
+  if (!(org > 0x1p-900 && org < 0x1p900)) return -1;
+  double mul = 1.0 / org;
+  d1 *= mul;
+  d2 *= mul;
+  e *= mul;
+  double vt00 = 1.0, vt01 = 0.0, vt10 = 0.0, vt11 = 1.0;
+  double sminoa = __builtin_fabs(d1);
+  if (sminoa != 0.0) {
+    double mu = __builtin_fabs(d2) * (sminoa / (sminoa + __builtin_fabs(e)));
+    if (mu < sminoa) sminoa = mu;
+  }
+  sminoa = sminoa / __builtin_sqrt(2.0);
+  double thresh = (tolmul * eps) * sminoa;
+  const double floor_ = 6.0 * (2.0 * (2.0 * unfl));
+  if (floor_ > thresh) thresh = floor_;
+  if (__builtin_fabs(e) > thresh) {
+    double ssmin, ssmax, snr, csr, snl, csl;
+    dlasv2(d1, e, d2, ssmin, ssmax, snr, csr, snl, csl);
+    d1 = ssmax;
+    d2 = ssmin;
+    double a0 = vt00, c0 = vt10;
+    vt00 = __builtin_fma(csr, a0, snr * c0);
+    vt10 = __builtin_fma(csr, c0, -(snr * a0));
+    double a1 = vt01, c1 = vt11;
+    vt01 = __builtin_fma(csr, a1, snr * c1);
+    vt11 = __builtin_fma(csr, c1, -(snr * a1));
+    double p = b1, q = b2;
+    b1 = __builtin_fma(csl, p, snl * q);
+    b2 = __builtin_fma(csl, q, -(snl * p));
+  }
+  if (d1 < 0.0) {
+    d1 = -d1;
+    vt00 = -vt00;
+    vt01 = -vt01;
+  }
+  if (d2 < 0.0) {
+    d2 = -d2;
+    vt10 = -vt10;
+    vt11 = -vt11;
+  }
+  // DBDSQR leaves them descending; DLASDQ re-sorts ascending. Net: one swap iff d1 > d2 after
+  // the descending sort, i.e. swap when d1 != d2 ends up with the larger first.
+  if (d2 > d1) {
+    double t = d1; d1 = d2; d2 = t;
+    t = vt00; vt00 = vt10; vt10 = t;
+    t = vt01; vt01 = vt11; vt11 = t;
+    t = b1; b1 = b2; b2 = t;
+  }
+  if (d2 < d1) {
+    double t = d1; d1 = d2; d2 = t;
+    t = vt00; vt00 = vt10; vt10 = t;
+    t = vt01; vt01 = vt11; vt11 = t;
+    t = b1; b1 = b2; b2 = t;
+  }
+  double dmax = __builtin_fabs(d1) > __builtin_fabs(d2) ? __builtin_fabs(d1) : __builtin_fabs(d2);
+  double tol2 = rcnd * dmax;
+  int rank = 0;
+  if (d1 <= tol2) {
+    b1 = 0.0;
+  } else {
+    b1 = b1 * (1.0 / d1);
+    rank++;
+  }
+  if (d2 <= tol2) {
+    b2 = 0.0;
+  } else {
+    b2 = b2 * (1.0 / d2);
+    rank++;
+  }
+  double s0 = __builtin_fma(vt10, b2, vt00 * b1);
+  double s1 = __builtin_fma(vt11, b2, vt01 * b1);
+  x0 = s0 * mul;
+  x1 = s1 * mul;
+  return rank;
+}
+
+// ------------------------------------------------------------------------------------------------
+// least_squares (utils.py:584-598) of one segment of m >= 2 points given by X(k), Y(k).
+// want_solution = false skips DLALSD (the DP needs only the residual; numpy still reports
+// residuals only at rank 2, which the segment's distinct x guarantee — checked by the caller via
+// lstsq_rank_ok when needed). Returns 0 on success, < 0 for paths not emulated.
+// ------------------------------------------------------------------------------------------------
+template <class GX, class GY>
+__host__ __device__ inline int lstsq_segment(int m, GX X, GY Y, bool want_solution, double& slope,
+                                             double& icpt, double& ssr) {
+  const double rcond = 0x1p-52 * (double)(m > 2 ? m : 2);
+  // DGELSD: B == 0 gives the zero solution at rank 0 (numpy then reports no residuals → 0.0);
+  // B or A outside [SMLNUM, BIGNUM] = [2^-970, 2^970] would be rescaled (not emulated).
+  {
+    double bnrm = 0.0, anrm = 1.0;
+    for (int k = 0; k < m; k++) {
+      bnrm = __builtin_fmax(bnrm, __builtin_fabs(Y(k)));
+      anrm = __builtin_fmax(anrm, __builtin_fabs(X(k)));
+    }
+    if (bnrm == 0.0) {
+      slope = 0.0;
+      icpt = 0.0;
+      ssr = 0.0;
+      return 0;
+    }
+    if (bnrm < 0x1p-970 || bnrm > 0x1p970 || anrm > 0x1p970) return -1;
+  }
+  // H1 = DLARFG(m, x0, x[1:])
+  double alpha = X(0);
+  double xn = nrm2(m - 1, [&](int k) { return X(k + 1); });
+  double tau1 = 0.0, beta1 = alpha, s1 = 0.0;
+  if (xn != 0.0) {
+    beta1 = -__builtin_copysign(dlapy2(alpha, xn), alpha);
+    tau1 = (beta1 - alpha) / beta1;
+    s1 = 1.0 / (alpha - beta1);
+  }
+  auto v1 = [&](int k) { return k == 0 ? 1.0 : X(k) * s1; };
+  // DLARF(v1, tau1) on the ones column and on y
+  int lastv = m;
+  double sc = 0.0, sb = 0.0;
+  bool c_upd = false, b_upd = false;
+  if (tau1 != 0.0) {
+    while (lastv > 1 && v1(lastv - 1) == 0.0) lastv--;
+    double w = gemv_t1(lastv, [](int) { return 1.0; }, v1);
+    sc = (-tau1) * w;
+    c_upd = true;
+    bool any = false;
+    for (int k = 0; k < lastv && !any; k++) any = Y(k) != 0.0;
+    if (any) {
+      double wb = gemv_t1(lastv, Y, v1);
+      sb = (-tau1) * wb;
+      b_upd = true;
+    }
+  }
+  auto C = [&](int k) { return (c_upd && k < lastv) ? __builtin_fma(sc, v1(k), 1.0) : 1.0; };
+  auto B = [&](int k) { return (b_upd && k < lastv) ? __builtin_fma(sb, v1(k), Y(k)) : Y(k); };
+  int rank;
+  double s0 = 0.0, sI = 0.0, res = 0.0;
+  if (m == 2) {
+    slope = 0.0;
+    icpt = 0.0;
+    ssr = 0.0;
+    if (!want_solution) return 0;
+    rank = dlalsd2(beta1, C(1), C(0), B(0), B(1), rcond, s0, sI);
+  } else {
+    double r12 = C(0);
+    double alpha2 = C(1);
+    double xn2 = nrm2(m - 2, [&](int k) { return C(k + 2); });
+    double tau2 = 0.0, beta2 = alpha2, s2 = 0.0;
+    if (xn2 != 0.0) {
+      beta2 = -__builtin_copysign(dlapy2(alpha2, xn2), alpha2);
+      tau2 = (beta2 - alpha2) / beta2;
+      s2 = 1.0 / (alpha2 - beta2);
+    }
+    // v2 over b[1:]: v2(0) = 1, v2(k) = c(k+1) * s2
+    auto v2 = [&](int k) { return k == 0 ? 1.0 : C(k + 1) * s2; };
+    int lastv2 = m - 1;
+    double sb2 = 0.0;
+    bool b2_upd = false;
+    if (tau2 != 0.0) {
+      while (lastv2 > 1 && v2(lastv2 - 1) == 0.0) lastv2--;
+      bool any = false;
+      for (int k = 0; k < lastv2 && !any; k++) any = B(k + 1) != 0.0;
+      if (any) {
+        double w2 = gemv_t1(lastv2, [&](int k) { return B(k + 1); }, v2);
+        sb2 = (-tau2) * w2;
+        b2_upd = true;
+      }
+    }
+    auto B2 = [&](int k) {  // final b (k >= 1)
+      double bk = B(k);
+      return (b2_upd && k - 1 < lastv2) ? __builtin_fma(sb2, v2(k - 1), bk) : bk;
+    };
+    for (int k = 2; k < m; k++) {
+      double bk = B2(k);
+      res = res + bk * bk;
+    }
+    if (!want_solution) {
+      slope = 0.0;
+      icpt = 0.0;
+      ssr = res;
+      return 0;
+    }
+    rank = dlalsd2(beta1, beta2, r12, B(0), B2(1), rcond, s0, sI);
+  }
+  if (rank < 0) return -1;
+  slope = s0;
+  icpt = sI;
+  ssr = (rank == 2 && m > 2) ? res : 0.0;
+  return rank == 2 ? 0 : -3;
+}
+
+}  // namespace lt

@@ -1,0 +1,89 @@
+"""Seeded synthetic Landsat-like scenes for tests, goldens and bench.py.
+
+A scene is a co-registered stack: every pixel sees the same acquisition dates (obs), so the
+observation metadata is per scene and the values / cloud masks are per pixel, stored obs-major
+([K][P], pixel index fastest) — the layout lt_analyze_tile consumes (include/lt_abi.h).
+
+Per pixel (integers, as a `B1 - B2` int16 index would give):
+  base ~ U{200..1500}; disturbance year d ~ U{3..T-5}; drop ~ U{100..800};
+  recovery slope ~ U{0..drop/10}, recovery capped at drop; noise round(N(0, 40));
+  spikes with probability 0.05 of +-U{200..1500}.
+Per year K_y ~ U{k_min..k_max} observations with day-of-year ~ U{120..270}; cloud mask 0 with
+probability `mask_prob` (masked obs are dropped, as apply_grid does, utils.py:350-354).
+Bands: B2 ~ U{100..400}, B1 = B2 + index, so `B1 - B2` reproduces the index exactly in int16.
+
+Everything is generated with torch on `device` (the bench builds 49 Mpx scenes directly in HBM).
+"""
+import datetime as _dt
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import torch
+
+
+@dataclass
+class Scene:
+    dates: List[_dt.date]              # [K] acquisition dates, in input (obs) order
+    values: torch.Tensor               # [K, P] float64 index values
+    valid: Optional[torch.Tensor]      # [K, P] uint8 (1 = keep), None = no cloud mask
+    bands: Optional[torch.Tensor] = None  # [K, 2, P] int16 (B1, B2) when requested
+    meta: dict = field(default_factory=dict)
+
+    @property
+    def n_obs(self):
+        return len(self.dates)
+
+    @property
+    def n_pix(self):
+        return self.values.shape[1]
+
+
+def make_scene(n_pix, n_years=30, k_min=1, k_max=1, mask_prob=0.0, first_year=1985, seed=0,
+               device='cpu', with_bands=False, spike_prob=0.05, chunk=1 << 22):
+    """Build a seeded synthetic scene. Deterministic for a given (seed, device type)."""
+    g_cpu = torch.Generator().manual_seed(int(seed))
+    # --- per-scene observation dates (obs order = ascending acquisition date) ---
+    dates = []
+    year_of_obs = []
+    for t in range(n_years):
+        k_y = int(torch.randint(k_min, k_max + 1, (1,), generator=g_cpu))
+        doys = sorted(int(v) for v in torch.randint(120, 271, (k_y,), generator=g_cpu))
+        for doy in doys:
+            dates.append(_dt.date(first_year + t, 1, 1) + _dt.timedelta(days=doy - 1))
+            year_of_obs.append(t)
+    K = len(dates)
+    dev = torch.device(device)
+    gen = torch.Generator(device=dev).manual_seed(int(seed) * 7919 + 17)
+    t_obs = torch.tensor(year_of_obs, dtype=torch.int32, device=dev)
+    values = torch.empty((K, n_pix), dtype=torch.float64, device=dev)
+    valid = torch.empty((K, n_pix), dtype=torch.uint8, device=dev) if mask_prob > 0 else None
+    bands = torch.empty((K, 2, n_pix), dtype=torch.int16, device=dev) if with_bands else None
+    for p0 in range(0, n_pix, chunk):
+        p1 = min(n_pix, p0 + chunk)
+        n = p1 - p0
+        base = torch.randint(200, 1501, (n,), generator=gen, device=dev, dtype=torch.int32)
+        d = torch.randint(3, max(4, n_years - 4), (n,), generator=gen, device=dev,
+                          dtype=torch.int32)
+        drop = torch.randint(100, 801, (n,), generator=gen, device=dev, dtype=torch.int32)
+        u = torch.rand((n,), generator=gen, device=dev, dtype=torch.float64)
+        slope = torch.floor(u * (drop // 10 + 1).double()).to(torch.int32)
+        rel = t_obs[:, None] - d[None, :]                                  # [K, n]
+        rec = torch.minimum(slope[None, :] * rel.clamp(min=0), drop[None, :])
+        clean = torch.where(rel < 0, base[None, :], base[None, :] - drop[None, :] + rec)
+        noise = torch.round(40.0 * torch.randn((K, n), generator=gen, device=dev,
+                                                dtype=torch.float64)).to(torch.int32)
+        sp = torch.rand((K, n), generator=gen, device=dev) < spike_prob
+        mag = torch.randint(200, 1501, (K, n), generator=gen, device=dev, dtype=torch.int32)
+        sign = torch.where(torch.rand((K, n), generator=gen, device=dev) < 0.5, -1, 1)
+        idx = clean + noise + torch.where(sp, sign * mag, torch.zeros_like(mag))
+        values[:, p0:p1] = idx.double()
+        if valid is not None:
+            valid[:, p0:p1] = (torch.rand((K, n), generator=gen, device=dev) >= mask_prob).to(
+                torch.uint8)
+        if bands is not None:
+            b2 = torch.randint(100, 401, (K, n), generator=gen, device=dev, dtype=torch.int32)
+            bands[:, 0, p0:p1] = (b2 + idx).to(torch.int16)
+            bands[:, 1, p0:p1] = b2.to(torch.int16)
+    return Scene(dates=dates, values=values, valid=valid, bands=bands,
+                 meta=dict(n_years=n_years, k_min=k_min, k_max=k_max, mask_prob=mask_prob,
+                           first_year=first_year, seed=seed))
