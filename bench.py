@@ -1,0 +1,206 @@
+"""Benchmark: full LandTrendr analyze + label of a Landsat-scene-sized stack per GPU.
+
+Metric (BASELINE.json): Mpixels/s of full analyze (30-yr series), whole job over all GPUs, with
+the FP64-VALU roofline fraction of the dominant kernel. Default workload = configs[1] (c2):
+7000 x 7000 px x 30 years, 1 obs/yr, one GD rule, line_cost 10, on one MI355X. Inputs are
+synthetic, generated directly in HBM before the timed region.
+
+A step = one pass of the hot path over the rank's whole scene, as a queue of pixel tiles
+(lt_analyze_tile launches on the current stream). Multi-GPU (torchrun, one process per GPU):
+each rank analyses its own scene (weak scaling, no data-path collective); with --gather the
+label rasters are then gathered to rank 0 over RCCL inside the step (the reference's
+output_reducer input).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from land_trendr_amd.engine import get_engine  # noqa: E402
+from land_trendr_amd.scene import build_scene, parse_date  # noqa: E402
+from land_trendr_amd.settings import compile_params  # noqa: E402
+from land_trendr_amd.synth import make_scene  # noqa: E402
+
+FP64_PEAK_TFLOPS = 78.6     # MI355X FP64 vector peak (spec)
+HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md chip-level parameters
+
+GD = [{'name': 'gd', 'val': 1, 'change_type': 'GD'}]
+C3_RULES = [{'name': 'fd', 'val': 2, 'change_type': 'FD', 'onset_year': ['>=', 1995],
+             'duration': ['<', 4]},
+            {'name': 'gd', 'val': 3, 'change_type': 'GD', 'pre_threshold': ['>', 500]},
+            {'name': 'ld', 'val': 4, 'change_type': 'LD', 'duration': ['>', 2]}]
+CONFIGS = {
+    'c2': dict(desc='c2: 7000x7000 px x 30 yr, 1 obs/yr, GD rule, line_cost 10', pixels=49_000_000,
+               years=30, k=(1, 1), mask=0.0, line_cost=10.0, rules=GD, mode='reference',
+               trendline=False),
+    'c3': dict(desc='c3: 7000x7000 px x 30 yr, 1-4 obs/yr + cloud masks, FD/GD/LD rules',
+               pixels=49_000_000, years=30, k=(1, 4), mask=0.2, line_cost=10.0, rules=C3_RULES,
+               mode='documented', trendline=False),
+    'c5': dict(desc='c5: 40-yr series, line_cost 1, full per-year trendline output',
+               pixels=49_000_000, years=40, k=(1, 1), mask=0.0, line_cost=1.0, rules=GD,
+               mode='reference', trendline=True),
+}
+
+
+def f_ref(n):
+    """Algorithmic FP64 flops per pixel of the reference algorithm."""
+    s3 = n * (n + 1) * (n + 2) // 6 - 3 * n + 2
+    return 20 * s3 + n * (n + 1) + 24 * n
+
+
+def bytes_per_pixel(cfg, n_obs, n_years):
+    inp = n_obs * 8 + (n_obs if cfg['mask'] > 0 else 0)          # f64 index values + mask
+    lab = len(cfg['rules']) * (1 + 4 + 4 + 4 + 8)                 # matched/class/onset/dur/mag
+    tl = n_years * (6 * 8 + 2 + 2) if cfg['trendline'] else 0     # 6 f64 + spike/vertex + winner
+    return inp + lab + 4                                          # + status
+
+
+def cpu_baseline(cfg, seconds):
+    """The oracle (C restatement, pthreads over all host cores) on a bounded sample."""
+    from oracle import oracle
+    threads = os.cpu_count() or 1
+    try:
+        threads = len(os.sched_getaffinity(0))
+    except AttributeError:
+        pass
+    threads = min(threads, 64)
+    sample = max(64, 16 * threads)
+    rate = None
+    while True:
+        sc = make_scene(sample, n_years=cfg['years'], k_min=cfg['k'][0], k_max=cfg['k'][1],
+                        mask_prob=cfg['mask'], seed=77, device='cpu')
+        meta = build_scene(sc.dates, parse_date('2014-07-01'))
+        params, _ = compile_params(cfg['line_cost'], cfg['rules'], cfg['mode'])
+        vals = sc.values.numpy()
+        valid = sc.valid.numpy() if sc.valid is not None else None
+        t0 = time.perf_counter()
+        oracle.analyze_tile(meta, params, vals, valid, n_threads=threads)
+        dt = time.perf_counter() - t0
+        rate = sample / dt
+        if dt >= 0.5 * seconds or sample >= 2_000_000:
+            break
+        sample = int(min(2_000_000, max(sample * 2, rate * seconds)))
+    return {'value': rate / 1e6, 'unit': 'Mpixels/s', 'cores': threads, 'kind': 'port',
+            'sample': '%d synthetic px of the same config, oracle/lt_oracle.c, %.1f s' % (sample, dt)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=3)
+    ap.add_argument('--warmup', type=int, default=1)
+    ap.add_argument('--config', default='c2', choices=sorted(CONFIGS))
+    ap.add_argument('--pixels', type=int, default=0, help='pixels per GPU (default: config)')
+    ap.add_argument('--tile', type=int, default=1 << 22, help='pixels per launch')
+    ap.add_argument('--gather', action='store_true', help='RCCL-gather label rasters to rank 0')
+    ap.add_argument('--cpu-seconds', type=float, default=15.0)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    args = ap.parse_args()
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    cfg = CONFIGS[args.config]
+    P = args.pixels or cfg['pixels']
+    dev = torch.device('cuda', local)
+
+    sc = make_scene(P, n_years=cfg['years'], k_min=cfg['k'][0], k_max=cfg['k'][1],
+                    mask_prob=cfg['mask'], seed=1000 + rank, device=dev)
+    meta = build_scene(sc.dates, parse_date('2014-07-01'))
+    params, rules = compile_params(cfg['line_cost'], cfg['rules'], cfg['mode'])
+    eng = get_engine(local)
+    fields = ['status', 'matched', 'class_val', 'onset_year', 'duration', 'magnitude']
+    if cfg['trendline']:
+        fields += ['winner', 'val_raw', 'val_fit', 'fit_m', 'fit_b', 'right_m', 'right_b',
+                   'spike', 'vertex']
+    out = eng.alloc_outputs(meta.n_years, params.n_rules, P, fields)
+    tiles = [(p0, min(P, p0 + args.tile)) for p0 in range(0, P, args.tile)]
+    gathered = None
+    if dist is not None and args.gather and rank == 0:
+        gathered = [torch.empty_like(out['class_val']) for _ in range(world)]
+
+    def step():
+        for p0, p1 in tiles:
+            view = {f: (t[..., p0:p1]) for f, t in out.items()}
+            eng.analyze_tile(meta, params, sc.values[:, p0:p1],
+                             sc.valid[:, p0:p1] if sc.valid is not None else None,
+                             fields, out=view)
+        if dist is not None and args.gather:
+            for f in ('class_val', 'onset_year', 'duration', 'magnitude'):
+                dist.gather(out[f], [torch.empty_like(out[f]) for _ in range(world)]
+                            if rank == 0 else None, dst=0)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    eng.set_timing(True)
+    eng.stage_ms()  # reset
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if dist is not None:
+        dist.barrier()
+    stages = eng.stage_ms()
+    eng.set_timing(False)
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    if dist is not None:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    elapsed = float(elapsed.item())
+
+    # correctness gate on this run's own outputs: no pixel may be flagged as an unemulated path
+    n_numeric = int(((out['status'] & 16) != 0).sum().item())
+
+    total_px = P * world * args.steps
+    value = total_px / elapsed / 1e6
+    n_launch = max(1, stages['launches'])
+    kern_ms = stages['analyze'] / n_launch
+    px_per_launch = P * args.steps / n_launch
+    flops = f_ref(cfg['years']) * px_per_launch
+    achieved = flops / (kern_ms * 1e-3) / 1e12
+    res = {
+        'metric': 'Mpixels/sec full analyze (30-yr series)' if cfg['years'] == 30 else
+                  'Mpixels/sec full analyze (%d-yr series)' % cfg['years'],
+        'value': round(value, 4), 'unit': 'Mpixels/s', 'n_gpus': world, 'steps': args.steps,
+        'warmup': args.warmup, 'ms_per_step': round(elapsed / args.steps * 1e3, 3),
+        'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f64',
+        'data': 'synthetic (SURVEY.md 8(d) generator, seeded, generated in HBM)',
+        'config': {'workload': cfg['desc'], 'pixels_per_gpu': P, 'years': cfg['years'],
+                   'obs': meta.n_obs, 'rules': len(rules), 'line_cost': cfg['line_cost'],
+                   'tile_pixels': args.tile, 'gather': bool(args.gather and world > 1),
+                   'parallelism': 'pixel tiles, 1 scene per GPU'},
+        'roofline': {'bound': 'fp64-valu', 'achieved': round(achieved, 3),
+                     'peak': FP64_PEAK_TFLOPS, 'unit': 'TFLOP/s',
+                     'frac': round(achieved / FP64_PEAK_TFLOPS, 4), 'traffic': None,
+                     'kernel': 'analyze_kernel', 'kernel_ms': round(kern_ms, 3),
+                     'flops_per_px': f_ref(cfg['years']),
+                     'algorithmic_bytes_per_px': bytes_per_pixel(cfg, meta.n_obs, meta.n_years),
+                     'hbm_gbs_algorithmic': round(bytes_per_pixel(cfg, meta.n_obs, meta.n_years)
+                                                  * px_per_launch / (kern_ms * 1e-3) / 1e9, 2)},
+        'status_numeric_pixels': n_numeric,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        res['cpu_baseline'] = cpu_baseline(cfg, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

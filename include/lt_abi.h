@@ -120,6 +120,17 @@ typedef struct {
   double* initial_val;
 } lt_tile_out;
 
+/* Input of the label stage alone: an already analysed trendline per pixel. */
+typedef struct {
+  int64_t n_pix;
+  int64_t stride;             /* elements between year planes                               */
+  int32_t n_years;            /* Y slots                                                    */
+  const int32_t* year;        /* [Y] HOST array: calendar year of each slot                 */
+  const double* val_fit;      /* [Y][stride] device                                         */
+  const uint8_t* vertex;      /* [Y][stride] device                                         */
+  const uint8_t* present;     /* [Y][stride] device, 0 = no point in this slot; NULL = all  */
+} lt_label_in;
+
 typedef struct lt_ctx lt_ctx;
 
 int lt_abi_version(void);
@@ -133,6 +144,11 @@ const char* lt_last_error(const lt_ctx* ctx);
  * fit / label kernel. */
 int lt_analyze_tile(lt_ctx* ctx, const lt_scene* scene, const lt_params* params,
                     const lt_tile_in* in, const lt_tile_out* out, void* stream);
+
+/* change_labeling alone (utils.py:795-820) on trendlines already in device memory. Writes the
+ * rule planes of `out` and out->status (only LT_ST_PRE_THRESHOLD_ATTR can be set). */
+int lt_label_tile(lt_ctx* ctx, const lt_label_in* in, const lt_params* params,
+                  const lt_tile_out* out, void* stream);
 
 /* Stage timing: when enabled, each lt_analyze_tile brackets its kernels with hipEvents on the
  * launch stream; lt_ctx_stage_ms returns the accumulated milliseconds per stage

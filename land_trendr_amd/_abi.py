@@ -62,6 +62,12 @@ class LtTileOut(ctypes.Structure):
                 ('initial_val', c_f64p)]
 
 
+class LtLabelIn(ctypes.Structure):
+    _fields_ = [('n_pix', ctypes.c_int64), ('stride', ctypes.c_int64),
+                ('n_years', ctypes.c_int32), ('year', c_i32p), ('val_fit', c_f64p),
+                ('vertex', c_u8p), ('present', c_u8p)]
+
+
 # per-year outputs [Y][stride] and per-rule outputs [R][stride]: (field, numpy dtype)
 YEAR_FIELDS = [('winner', 'int16'), ('val_raw', 'float64'), ('val_fit', 'float64'),
                ('fit_m', 'float64'), ('fit_b', 'float64'), ('right_m', 'float64'),
@@ -72,7 +78,7 @@ PIX_FIELDS = [('status', 'int32'), ('n_years', 'int32')]
 
 # symbols include/lt_abi.h declares (checked by tests/test_abi.py)
 EXPORTS = ['lt_abi_version', 'lt_ctx_create', 'lt_ctx_destroy', 'lt_last_error',
-           'lt_analyze_tile', 'lt_ctx_set_timing', 'lt_ctx_stage_ms']
+           'lt_analyze_tile', 'lt_label_tile', 'lt_ctx_set_timing', 'lt_ctx_stage_ms']
 
 _LIB = None
 
@@ -95,6 +101,8 @@ def load_lib(path=None):
     lib.lt_last_error.restype = ctypes.c_char_p
     lib.lt_analyze_tile.argtypes = [vp, ctypes.POINTER(LtScene), ctypes.POINTER(LtParams),
                                     ctypes.POINTER(LtTileIn), ctypes.POINTER(LtTileOut), vp]
+    lib.lt_label_tile.argtypes = [vp, ctypes.POINTER(LtLabelIn), ctypes.POINTER(LtParams),
+                                  ctypes.POINTER(LtTileOut), vp]
     lib.lt_ctx_set_timing.argtypes = [vp, ctypes.c_int]
     lib.lt_ctx_stage_ms.argtypes = [vp, c_f64p, ctypes.c_int, ctypes.POINTER(ctypes.c_int64)]
     if lib.lt_abi_version() != LT_ABI_VERSION:

@@ -1,0 +1,338 @@
+// lt_pixel.h — the per-pixel LandTrendr pipeline as device code (one pixel per lane).
+//
+// Stages, in reference order (/root/reference/utils.py):
+//   pick_winners :491-521   winner per calendar year (scene metadata in scalar memory)
+//   despike      :556-582   numpy-pairwise std + 3-window scan over the ORIGINAL series
+//   timeseries2int_series :534-554, dropna :608
+//   segmented_least_squares :600-631 + find_segments :633-644   (DP, first-minimum argmin)
+//   vertices2eqns :646-669, eqns2fitted_points :682-722
+//   Trendline.parse_disturbances / match_rule (classes.py:156-232), change_labeling :795-820
+// All arithmetic that can decide a tie is the emulated LAPACK of lt_lapack.h.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/lt_abi.h"
+#include "lt_lapack.h"
+
+namespace lt {
+
+// Scene metadata in device memory (uploaded once per distinct scene by lt_analyze_tile).
+struct DevScene {
+  int32_t n_obs;
+  int32_t n_years;
+  int32_t year[LT_MAX_YEARS];
+  int32_t slot_begin[LT_MAX_YEARS + 1];
+  uint8_t feb29_bad[LT_MAX_YEARS];
+  int32_t order[LT_MAX_OBS];
+  int32_t dist[LT_MAX_OBS];
+};
+
+// numpy pairwise sum (n <= 128) of a[0..n-1]: 8 accumulators, then sequential remainder.
+template <class G>
+__device__ inline double np_sum(int n, G a) {
+  if (n < 8) {
+    double r = 0.0;
+    for (int i = 0; i < n; i++) r += a(i);
+    return r;
+  }
+  double r0 = a(0), r1 = a(1), r2 = a(2), r3 = a(3), r4 = a(4), r5 = a(5), r6 = a(6), r7 = a(7);
+  int i = 8;
+  for (; i < n - (n % 8); i += 8) {
+    r0 += a(i); r1 += a(i + 1); r2 += a(i + 2); r3 += a(i + 3);
+    r4 += a(i + 4); r5 += a(i + 5); r6 += a(i + 6); r7 += a(i + 7);
+  }
+  double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+  for (; i < n; i++) res += a(i);
+  return res;
+}
+
+// change_labeling state for all rules (classes.py:213-230 winner bookkeeping).
+struct RuleState {
+  bool have[LT_MAX_RULES];
+  int32_t on[LT_MAX_RULES], du[LT_MAX_RULES];
+  double mag[LT_MAX_RULES], init[LT_MAX_RULES];
+
+  __device__ void reset(int nr) {
+    for (int r = 0; r < nr; r++) {
+      have[r] = false;
+      on[r] = LT_NODATA;
+      du[r] = LT_NODATA;
+      mag[r] = (double)LT_NODATA;
+      init[r] = (double)LT_NODATA;
+    }
+  }
+
+  // One Disturbance (classes.py:170-175) offered to every rule: match_rule's filters
+  // (classes.py:190-211) then the FD/GD/LD replacement on strict inequality (:217-230).
+  __device__ void offer(const lt_params& P, int32_t d_on, int32_t d_du, double d_init,
+                        double d_mag, int& status) {
+    for (int r = 0; r < P.n_rules; r++) {
+      const lt_rule& R = P.rules[r];
+      bool match = true;
+      if (R.onset_op == LT_Q_EQ) match = match && ((double)d_on == R.onset_val);
+      else if (R.onset_op == LT_Q_LE) match = match && !((double)d_on > R.onset_val);
+      else if (R.onset_op == LT_Q_GE) match = match && !((double)d_on < R.onset_val);
+      if (R.duration_op == LT_Q_GT) match = match && !((double)d_du <= R.duration_val);
+      else if (R.duration_op == LT_Q_LT) match = match && !((double)d_du >= R.duration_val);
+      if (R.pre_op != LT_Q_UNSET) {
+        if (P.pre_threshold_mode == LT_PRE_REFERENCE) status |= LT_ST_PRE_THRESHOLD_ATTR;
+        else if (R.pre_op == LT_Q_GT) match = match && !(d_init <= R.pre_val);
+        else if (R.pre_op == LT_Q_LT) match = match && !(d_init >= R.pre_val);
+      }
+      if (!match) continue;
+      bool take = !have[r];
+      if (have[r]) {
+        if (R.change_type == LT_CT_FD) take = d_on < on[r];
+        else if (R.change_type == LT_CT_GD) take = d_mag > mag[r];
+        else if (R.change_type == LT_CT_LD) take = d_du > du[r];
+      }
+      if (take) {
+        have[r] = true;
+        on[r] = d_on;
+        du[r] = d_du;
+        mag[r] = d_mag;
+        init[r] = d_init;
+      }
+    }
+  }
+
+  __device__ void write(const lt_params& P, const lt_tile_out& out, int64_t p) const {
+    const int64_t os = out.stride;
+    for (int r = 0; r < P.n_rules; r++) {
+      const int64_t q = (int64_t)r * os + p;
+      if (out.matched) out.matched[q] = have[r] ? 1 : 0;
+      if (out.class_val) out.class_val[q] = have[r] ? P.rules[r].class_val : LT_NODATA;
+      if (out.onset_year) out.onset_year[q] = on[r];
+      if (out.duration) out.duration[q] = du[r];
+      if (out.magnitude) out.magnitude[q] = mag[r];
+      if (out.initial_val) out.initial_val[q] = init[r];
+    }
+  }
+};
+
+template <int MAXY>
+__device__ void analyze_pixel(const DevScene& S, const lt_params& P, const lt_tile_in& in,
+                              const lt_tile_out& out, int64_t p) {
+  const int Y = S.n_years;
+  const int64_t is = in.stride, os = out.stride;
+  int status = LT_ST_OK;
+
+  // ---- pick_winners: per year slot, first valid obs (input order) at minimal |days| ----
+  double val[MAXY];
+  uint8_t slot[MAXY];
+  int T = 0;
+  for (int y = 0; y < Y; y++) {
+    int best = -1, bd = 0x7fffffff;
+    const int k1 = S.slot_begin[y + 1];
+    for (int k = S.slot_begin[y]; k < k1; k++) {
+      const int o = S.order[k];
+      const bool ok = in.obs_valid == nullptr || in.obs_valid[(int64_t)o * is + p] != 0;
+      if (ok && S.dist[k] < bd) {
+        bd = S.dist[k];
+        best = o;
+      }
+    }
+    if (out.winner) out.winner[(int64_t)y * os + p] = (int16_t)best;
+    if (best >= 0) {
+      if (S.feb29_bad[y]) status |= LT_ST_FEB29;
+      val[T] = in.obs_val[(int64_t)best * is + p];
+      slot[T] = (uint8_t)y;
+      T++;
+    }
+  }
+  if (out.n_years) out.n_years[p] = T;
+  const int y0 = T > 0 ? S.year[slot[0]] : 0;
+
+  uint64_t spike_m = 0;  // bits over the T-point series
+  const bool ok = T >= 2;
+  if (T == 0) status |= LT_ST_EMPTY;
+  if (T == 1) status |= LT_ST_SINGLE_YEAR;
+  const double nan = __builtin_nan("");
+
+  // per-year outputs of absent years (and of every year when the reference raises)
+  {
+    int t = 0;
+    for (int y = 0; y < Y; y++) {
+      const bool present = t < T && slot[t] == y;
+      const int64_t q = (int64_t)y * os + p;
+      if (!present || !ok) {
+        if (out.val_raw) out.val_raw[q] = present ? val[t] : nan;
+        if (out.val_fit) out.val_fit[q] = nan;
+        if (out.fit_m) out.fit_m[q] = nan;
+        if (out.fit_b) out.fit_b[q] = nan;
+        if (out.right_m) out.right_m[q] = nan;
+        if (out.right_b) out.right_b[q] = nan;
+        if (out.spike) out.spike[q] = 0;
+        if (out.vertex) out.vertex[q] = 0;
+      }
+      if (present) t++;
+    }
+  }
+
+  RuleState rs;
+  rs.reset(P.n_rules);
+
+  if (ok) {
+    // ---- despike (utils.py:556-582) ----
+    const double avg = np_sum(T, [&](int i) { return val[i]; }) / (double)T;
+    const double sd = __builtin_sqrt(np_sum(T, [&](int i) {
+                                       double d = avg - val[i];
+                                       return d * d;
+                                     }) /
+                                     (double)T);
+    double last_good = val[0];
+    for (int i = 1; i < T - 1; i++) {
+      const double xv = val[i - 1], yv = val[i], zv = val[i + 1];
+      const bool mono = (xv <= yv && yv <= zv) || (xv >= yv && yv >= zv);
+      if (!mono && (__builtin_fabs(yv - xv) > sd && __builtin_fabs(yv - zv) > sd) &&
+          yv != last_good) {
+        spike_m |= 1ull << i;
+      } else {
+        last_good = yv;
+      }
+    }
+    // ---- dropna: the non-spike series (x = year offset) ----
+    double ys[MAXY];
+    uint8_t xs[MAXY];
+    int n = 0;
+    for (int i = 0; i < T; i++) {
+      if ((spike_m >> i) & 1) continue;
+      xs[n] = (uint8_t)(S.year[slot[i]] - y0);
+      ys[n] = val[i];
+      n++;
+    }
+    // ---- segmented least squares DP (utils.py:618-631) ----
+    double OPT[MAXY + 1];
+    uint8_t arg[MAXY];
+    OPT[0] = 0.0;
+    for (int j = 0; j < n; j++) {
+      double best = 0.0;
+      int bi = -1;
+      for (int i = 0; i <= j; i++) {
+        double e = 0.0;
+        if (i != j) {
+          double sm, sb, ssr;
+          int rc = lstsq_segment(
+              j - i + 1, [&](int k) { return (double)xs[i + k]; },
+              [&](int k) { return ys[i + k]; }, false, sm, sb, ssr);
+          if (rc < 0) status |= LT_ST_NUMERIC;
+          e = ssr;
+        }
+        const double v = (e + P.line_cost) + OPT[i];
+        if (bi < 0 || v < best) {
+          best = v;
+          bi = i;
+        }
+      }
+      OPT[j + 1] = best;
+      arg[j] = (uint8_t)bi;
+    }
+    // ---- find_segments: starts of the optimal segments + the last point ----
+    uint64_t vnon = 1ull << (n - 1);  // over non-spike indices
+    for (int j = n - 1; j >= 0; j = arg[j] - 1) vnon |= 1ull << arg[j];
+
+    // ---- vertices2eqns + eqns2fitted_points + labels, walking the full series ----
+    double cm = 0.0, cb = 0.0;  // eqn of the current (most recent) vertex
+    int k = 0;                  // non-spike index
+    double left_fit = 0.0;
+    int32_t left_year = y0;
+    for (int i = 0; i < T; i++) {
+      const bool sp = (spike_m >> i) & 1;
+      bool is_v = false;
+      const double pm = cm, pb = cb;  // left eqn = previous point's right eqn
+      if (!sp) {
+        if ((vnon >> k) & 1) {
+          is_v = true;
+          const uint64_t later = vnon & ~((2ull << k) - 1);
+          if (later) {  // not the last vertex: LS over [k, next vertex] (label-inclusive)
+            const int k2 = __builtin_ctzll(later);
+            double sm, sb, ssr;
+            int rc = lstsq_segment(
+                k2 - k + 1, [&](int q) { return (double)xs[k + q]; },
+                [&](int q) { return ys[k + q]; }, true, sm, sb, ssr);
+            if (rc < 0) status |= LT_ST_NUMERIC;
+            cm = sm;
+            cb = sb;
+          }  // last vertex reuses the previous vertex's eqn (utils.py:662)
+        }
+        k++;
+      }
+      const int32_t yr = S.year[slot[i]];
+      const double x = (double)(yr - y0);
+      double fv, fmv, fbv;
+      if (i == 0 || (pm == cm && pb == cb)) {
+        fv = (cm * x) + cb;
+        fmv = cm;
+        fbv = cb;
+      } else {
+        const double fl = (pm * x) + pb;
+        const double fr = (cm * x) + cb;
+        const double raw = sp ? nan : val[i];
+        if (__builtin_fabs(fl - raw) <= __builtin_fabs(fr - raw)) {
+          fv = fl; fmv = pm; fbv = pb;
+        } else {
+          fv = fr; fmv = cm; fbv = cb;
+        }
+      }
+      const int64_t q = (int64_t)slot[i] * os + p;
+      if (out.val_raw) out.val_raw[q] = val[i];
+      if (out.val_fit) out.val_fit[q] = fv;
+      if (out.fit_m) out.fit_m[q] = fmv;
+      if (out.fit_b) out.fit_b[q] = fbv;
+      if (out.right_m) out.right_m[q] = cm;
+      if (out.right_b) out.right_b[q] = cb;
+      if (out.spike) out.spike[q] = sp ? 1 : 0;
+      if (out.vertex) out.vertex[q] = is_v ? 1 : 0;
+
+      // parse_disturbances (classes.py:156-176): the first point is the first left vertex
+      if (i == 0) {
+        left_fit = fv;
+        left_year = yr;
+      } else if (is_v) {
+        const int32_t on = left_year;
+        const int32_t du = yr - left_year;
+        const double init = left_fit;
+        const double mag = left_fit - fv;
+        left_fit = fv;
+        left_year = yr;
+        rs.offer(P, on, du, init, mag, status);
+      }
+    }
+  }
+
+  rs.write(P, out, p);
+  if (out.status) out.status[p] = status;
+}
+
+// Label stage alone (change_labeling on an existing trendline): per slot y, val_fit / vertex /
+// present planes; the first present point is the first left vertex (classes.py:163-164).
+__device__ inline void label_pixel(const int32_t* year, int Y, const lt_params& P,
+                                   const lt_label_in& in, const lt_tile_out& out, int64_t p) {
+  const int64_t is = in.stride;
+  int status = LT_ST_OK;
+  RuleState rs;
+  rs.reset(P.n_rules);
+  bool first = true;
+  double left_fit = 0.0;
+  int32_t left_year = 0;
+  for (int y = 0; y < Y; y++) {
+    const int64_t q = (int64_t)y * is + p;
+    if (in.present && !in.present[q]) continue;
+    const double fv = in.val_fit[q];
+    if (first) {
+      first = false;
+      left_fit = fv;
+      left_year = year[y];
+      continue;
+    }
+    if (!in.vertex[q]) continue;
+    rs.offer(P, left_year, year[y] - left_year, left_fit, left_fit - fv, status);
+    left_fit = fv;
+    left_year = year[y];
+  }
+  rs.write(P, out, p);
+  if (out.status) out.status[p] = status;
+}
+
+}  // namespace lt

@@ -1,0 +1,164 @@
+"""Tile engine: torch device tensors in, lt_analyze_tile (HIP) on the current stream, tensors out.
+
+One Engine per GPU (per process). torch provides device memory and the stream only; all compute
+happens in land_trendr_amd/liblt_hip.so. There is no CPU path.
+"""
+import ctypes
+
+import torch
+
+from . import _abi
+
+TRENDLINE = tuple(f for f, _ in _abi.YEAR_FIELDS)
+LABELS = tuple(f for f, _ in _abi.RULE_FIELDS)
+ALL_FIELDS = TRENDLINE + LABELS + ('status', 'n_years')
+LABEL_FIELDS = ('status', 'matched', 'class_val', 'onset_year', 'duration', 'magnitude')
+
+_DT = {'int16': torch.int16, 'int32': torch.int32, 'uint8': torch.uint8,
+       'float64': torch.float64}
+_SHAPE_KIND = {**{f: 'year' for f, _ in _abi.YEAR_FIELDS},
+               **{f: 'rule' for f, _ in _abi.RULE_FIELDS},
+               **{f: 'pix' for f, _ in _abi.PIX_FIELDS}}
+_DTYPE = {f: _DT[d] for f, d in _abi.YEAR_FIELDS + _abi.RULE_FIELDS + _abi.PIX_FIELDS}
+
+
+class LtError(RuntimeError):
+    pass
+
+
+class Engine:
+    def __init__(self, device=None):
+        if not torch.cuda.is_available():
+            raise LtError('land_trendr_amd needs a HIP device (no CPU fallback)')
+        self.lib = _abi.load_lib()
+        self.device = torch.device('cuda', torch.cuda.current_device() if device is None
+                                   else int(device))
+        ctx = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            rc = self.lib.lt_ctx_create(self.device.index, ctypes.byref(ctx))
+        if rc != 0:
+            raise LtError('lt_ctx_create failed (%d)' % rc)
+        self.ctx = ctx
+
+    def close(self):
+        if self.ctx:
+            self.lib.lt_ctx_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        if rc != 0:
+            raise LtError('%s failed (%d): %s' % (what, rc,
+                                                  self.lib.lt_last_error(self.ctx).decode()))
+
+    def alloc_outputs(self, n_years, n_rules, n_pix, fields=ALL_FIELDS):
+        out = {}
+        for f in fields:
+            kind = _SHAPE_KIND[f]
+            shape = {'year': (n_years, n_pix), 'rule': (max(n_rules, 1), n_pix),
+                     'pix': (n_pix,)}[kind]
+            out[f] = torch.empty(shape, dtype=_DTYPE[f], device=self.device)
+        return out
+
+    def analyze_tile(self, scene, params, values, valid=None, fields=ALL_FIELDS, out=None,
+                     stream=None):
+        """values: float64 [K, P] (or a [K, stride] view's base), valid: uint8 [K, P] or None.
+        Returns the dict of output tensors ([Y, P], [R, P], [P]); asynchronous on `stream`."""
+        if values.dtype != torch.float64 or values.device != self.device or values.dim() != 2:
+            raise LtError('values must be a float64 [K, P] tensor on %s' % self.device)
+        if values.stride(1) != 1:
+            raise LtError('values must have unit pixel stride')
+        K, P = values.shape
+        if K != scene.n_obs:
+            raise LtError('values has %d obs rows, scene has %d' % (K, scene.n_obs))
+        if valid is not None:
+            if (valid.dtype != torch.uint8 or valid.shape != values.shape or
+                    valid.stride() != values.stride() or valid.device != self.device):
+                raise LtError('valid must be uint8 with the shape/strides of values')
+        if out is None:
+            out = self.alloc_outputs(scene.n_years, params.n_rules, P, fields)
+        ostride = None
+        for f, t in out.items():
+            kind = _SHAPE_KIND[f]
+            if t.device != self.device or t.dtype != _DTYPE[f] or t.shape[-1] < P:
+                raise LtError('output %s has wrong device/dtype/shape' % f)
+            if kind != 'pix':
+                need = scene.n_years if kind == 'year' else params.n_rules
+                if t.shape[0] < need or t.stride(1) != 1:
+                    raise LtError('output %s too small' % f)
+                s = t.stride(0)
+                if ostride is None:
+                    ostride = s
+                elif s != ostride:
+                    raise LtError('all [Y|R, P] outputs must share one row stride')
+        tin = _abi.LtTileIn()
+        tin.n_pix = P
+        tin.stride = values.stride(0)
+        tin.obs_val = ctypes.cast(values.data_ptr(), _abi.c_f64p)
+        tin.obs_valid = ctypes.cast(valid.data_ptr(), _abi.c_u8p) if valid is not None else None
+        tout = _abi.LtTileOut()
+        tout.stride = ostride if ostride is not None else P
+        for f, t in out.items():
+            setattr(tout, f, ctypes.cast(t.data_ptr(), type(getattr(tout, f))))
+        sc = scene.to_c()
+        st = stream if stream is not None else torch.cuda.current_stream(self.device)
+        rc = self.lib.lt_analyze_tile(self.ctx, ctypes.byref(sc), ctypes.byref(params),
+                                      ctypes.byref(tin), ctypes.byref(tout),
+                                      ctypes.c_void_p(st.cuda_stream))
+        self._check(rc, 'lt_analyze_tile')
+        return out
+
+    # --- stage timing (HIP events recorded around every launch on the launch stream) ---
+    def set_timing(self, enable):
+        self._check(self.lib.lt_ctx_set_timing(self.ctx, 1 if enable else 0), 'set_timing')
+
+    def stage_ms(self):
+        ms = (ctypes.c_double * 2)()
+        n = ctypes.c_int64()
+        self._check(self.lib.lt_ctx_stage_ms(self.ctx, ms, 2, ctypes.byref(n)), 'stage_ms')
+        return {'winner': ms[0], 'analyze': ms[1], 'launches': n.value}
+
+
+_ENGINES = {}
+
+
+def get_engine(device=None):
+    idx = torch.cuda.current_device() if device is None else int(device)
+    eng = _ENGINES.get(idx)
+    if eng is None:
+        eng = _ENGINES[idx] = Engine(idx)
+    return eng
+
+
+def label_tile(engine, years, params, val_fit, vertex, present=None, out=None, stream=None):
+    """change_labeling alone on trendlines in device memory: val_fit float64 [Y, P],
+    vertex / present uint8 [Y, P] (same strides). Returns the rule-plane dict + status."""
+    import numpy as np
+    Y, P = val_fit.shape
+    yrs = np.ascontiguousarray(np.asarray(years, np.int32))
+    if len(yrs) != Y:
+        raise LtError('years must have one entry per slot')
+    if out is None:
+        out = engine.alloc_outputs(Y, params.n_rules, P, LABELS + ('status',))
+    lin = _abi.LtLabelIn()
+    lin.n_pix = P
+    lin.stride = val_fit.stride(0)
+    lin.n_years = Y
+    lin.year = yrs.ctypes.data_as(_abi.c_i32p)
+    lin.val_fit = ctypes.cast(val_fit.data_ptr(), _abi.c_f64p)
+    lin.vertex = ctypes.cast(vertex.data_ptr(), _abi.c_u8p)
+    lin.present = ctypes.cast(present.data_ptr(), _abi.c_u8p) if present is not None else None
+    tout = _abi.LtTileOut()
+    tout.stride = out['matched'].stride(0)
+    for f, t in out.items():
+        setattr(tout, f, ctypes.cast(t.data_ptr(), type(getattr(tout, f))))
+    st = stream if stream is not None else torch.cuda.current_stream(engine.device)
+    rc = engine.lib.lt_label_tile(engine.ctx, ctypes.byref(lin), ctypes.byref(params),
+                                  ctypes.byref(tout), ctypes.c_void_p(st.cuda_stream))
+    engine._check(rc, 'lt_label_tile')
+    return out

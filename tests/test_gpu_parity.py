@@ -1,0 +1,197 @@
+"""GPU parity: the HIP kernels (through the C ABI) against the reference goldens and the oracle.
+
+Bar: bit-exact for every integer and floating output; the north_star's 1e-9
+relative tolerance for fitted values / magnitude is not needed because the emulated LAPACK
+arithmetic reproduces the reference bits.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import golden_io
+from land_trendr_amd import _abi
+from land_trendr_amd.scene import build_scene, parse_date
+from land_trendr_amd.settings import compile_params
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope='module')
+def engine():
+    from land_trendr_amd.engine import get_engine
+    return get_engine(0)
+
+
+def _run(engine, g_scene, params, values, valid):
+    dev = engine.device
+    v = torch.from_numpy(np.ascontiguousarray(values)).to(dev)
+    m = torch.from_numpy(np.ascontiguousarray(valid)).to(dev) if valid is not None else None
+    out = engine.analyze_tile(g_scene, params, v, m)
+    torch.cuda.synchronize()
+    return {k: t.cpu().numpy() for k, t in out.items()}
+
+
+@pytest.mark.parametrize('name', golden_io.scene_names())
+def test_golden_scene_bit_exact(engine, name):
+    g = golden_io.GoldenScene(name)
+    out = _run(engine, g.scene, g.params, g.values, g.valid)
+    bad = golden_io.compare(g, out)
+    assert not bad, '\n'.join(bad[:40])
+
+
+def _synthetic_vs_oracle(engine, n_pix, seed, line_cost, rules, mode, **kw):
+    from land_trendr_amd.synth import make_scene
+    from oracle import oracle
+    sc = make_scene(n_pix, seed=seed, **kw)
+    meta = build_scene(sc.dates, parse_date('2014-07-01'))
+    params, _ = compile_params(line_cost, rules, mode)
+    vals = sc.values.numpy()
+    valid = sc.valid.numpy() if sc.valid is not None else None
+    got = _run(engine, meta, params, vals, valid)
+    want = oracle.analyze_tile(meta, params, vals, valid, n_threads=os.cpu_count() or 1)
+    for f in want:
+        a, b = want[f], got[f]
+        if a.dtype.kind == 'f':
+            same = (a.view(np.int64) == b.view(np.int64)) | (np.isnan(a) & np.isnan(b))
+        else:
+            same = a == b
+        assert same.all(), '%s: %d of %d differ' % (f, (~same).sum(), same.size)
+    return got
+
+
+def test_synthetic_c3_masks_vs_oracle(engine):
+    rules = [{'name': 'fd', 'val': 2, 'change_type': 'FD', 'onset_year': ['>=', 1995],
+              'duration': ['<', 4]},
+             {'name': 'gd', 'val': 3, 'change_type': 'GD', 'pre_threshold': ['>', 500]},
+             {'name': 'ld', 'val': 4, 'change_type': 'LD', 'duration': ['>', 2]}]
+    got = _synthetic_vs_oracle(engine, 20000, 103, 10, rules, 'documented', n_years=30,
+                               k_min=1, k_max=4, mask_prob=0.2)
+    assert (got['status'] == 0).mean() > 0.99
+
+
+def test_synthetic_c5_t40_low_cost_vs_oracle(engine):
+    _synthetic_vs_oracle(engine, 8000, 105, 1.0, [{'name': 'gd', 'val': 1, 'change_type': 'GD'}],
+                         'reference', n_years=40)
+
+
+def test_strided_tile_and_subset_outputs(engine):
+    """Tiles carved from a larger stack (stride > n_pix) and NULL outputs."""
+    g = golden_io.GoldenScene('c1')
+    dev = engine.device
+    K, P = g.values.shape
+    big = torch.zeros((K, P + 77), dtype=torch.float64, device=dev)
+    big[:, :P] = torch.from_numpy(g.values).to(dev)
+    view = big[:, :P]
+    out = engine.analyze_tile(g.scene, g.params, view, None,
+                              fields=('status', 'matched', 'magnitude'))
+    torch.cuda.synchronize()
+    mag = out['magnitude'].cpu().numpy()
+    assert golden_io._bits_equal(mag, g.ref['magnitude']).all()
+    assert (out['matched'].cpu().numpy() == g.ref['matched']).all()
+
+
+# ---- drop-in API (land_trendr_amd.utils mirrors /root/reference/utils.py) ----
+
+def test_reference_trendline_match_known_answer(engine):
+    """classes_test.py:35-62 (TrendLineTestCase.test_match) through the drop-in API."""
+    from land_trendr_amd import utils
+    from land_trendr_amd.classes import LabelRule
+    values = [{'date': '%d-12-31' % y, 'val': v} for y, v in
+              zip(range(2010, 2020), [10, 10, 10, 5, 5, 5, 7, 9, 10, 10])]
+    rule = LabelRule({'name': 'fast_dist', 'val': 2, 'change_type': 'GD',
+                      'duration': ['<', 4]})
+    tl = utils.analyze(values, 2, utils.parse_date('2014-07-01'))
+    match = tl.match_rule(rule)
+    assert match is not None
+    assert match.onset_year == 2010
+    assert round(match.initial_val - 10.999999999, 7) == 0
+    assert round(match.magnitude - 6.3999999999999, 7) == 0
+    assert match.duration == 3
+
+
+def test_reference_despike_and_segments_known_answers(engine):
+    """utils_test.py:161-189: despike flags and segmented-least-squares vertex lists."""
+    from land_trendr_amd import utils
+    t = utils.parse_date('2014-07-01')
+    yearly = lambda vals: [{'date': '%d-12-31' % (2010 + i), 'val': v}
+                           for i, v in enumerate(vals)]
+    tl = utils.analyze(yearly([1, 1, 1, 5, 1, 1, 1]), 1e-4, t)
+    assert [p.spike for p in tl.points] == [False, False, False, True, False, False, False]
+    tl = utils.analyze(yearly([1, 3, 1, 5, 1, 1, 1]), 1e-4, t)
+    assert [p.spike for p in tl.points] == [False, True, False, True, False, False, False]
+    tl = utils.analyze(yearly([0, 0, 0, 1, 2, 3]), 0.0001, t)
+    assert [p.index_day for p in tl.points if p.vertex] == [0, 2, 5]
+    tl = utils.analyze(yearly([0, 0, 0, 1, 1, 1, 3, 3]), 0.0001, t)
+    assert [p.index_day for p in tl.points if p.vertex] == [0, 3, 6, 7]
+
+
+def test_mr_label_output_matches_reference(engine):
+    from land_trendr_amd import utils
+    with open(os.path.join(golden_io.GOLDEN, 'mr_output.json')) as fh:
+        gold = json.load(fh)
+    g = golden_io.GoldenScene(gold['scene'])
+    for p, want in zip(gold['pixels'], gold['outputs']):
+        pdl = [{'date': g.meta['dates'][k], 'val': float(g.values[k, p])}
+               for k in range(g.values.shape[0])]
+        tl = utils.analyze(pdl, 10, utils.parse_date('2014-07-01'))
+        got = tl.mr_label_output()
+        assert sorted(got) == sorted(want)
+        for k in want:
+            assert golden_io._bits_equal(float(got[k]), want[k]), k
+
+
+def test_reference_error_types(engine):
+    from land_trendr_amd import utils
+    from land_trendr_amd.classes import LabelRule
+    t = utils.parse_date('2014-07-01')
+    with pytest.raises(IndexError):
+        utils.analyze([], 10, t)
+    with pytest.raises(ValueError):
+        utils.analyze([{'date': '2001-07-01', 'val': 3.0}], 10, t)
+    with pytest.raises(ValueError):
+        utils.analyze([{'date': '2001-07-01', 'val': 3.0}, {'date': '2002-07-01', 'val': 3.0}],
+                      10, utils.parse_date('2012-02-29'))
+    with pytest.raises(ValueError):
+        utils.analyze([{'date': '2001/07/01', 'val': 3.0}], 10, t)
+    tl = utils.analyze([{'date': '%d-07-01' % y, 'val': float(y % 7)} for y in range(2000, 2010)],
+                       10, t)
+    rule = LabelRule({'name': 'x', 'val': 1, 'change_type': 'GD', 'pre_threshold': ['>', 5]})
+    with pytest.raises(AttributeError):
+        utils.change_labeling(tl, [rule])
+    got = utils.change_labeling(tl, [rule], pre_threshold_mode='documented')
+    assert isinstance(got, dict)
+
+
+def test_analysis_reducer_key_format(engine):
+    from land_trendr_amd import utils
+    settings = {'line_cost': 10, 'target_date': '2014-07-01',
+                'label_rules': [{'name': 'gd', 'val': 1, 'change_type': 'GD'}]}
+    pdl = [{'date': '%d-07-01' % y, 'val': float(v)} for y, v in
+           zip(range(2000, 2012), [500, 510, 505, 520, 300, 330, 360, 390, 420, 800, 450, 470])]
+    out = list(utils.analysis_reducer('POINT(1 2)', pdl, settings))
+    keys = [k for k, _ in out]
+    assert keys[0] == 'trendline/2000-07-01-val_raw'
+    assert len([k for k in keys if k.startswith('trendline/')]) == 12 * 8
+    assert keys[-4:] == ['gd_class_val', 'gd_onset_year', 'gd_magnitude', 'gd_duration']
+    assert all(v['pix_ctr_wkt'] == 'POINT(1 2)' for _, v in out)
+    d = dict(out)
+    assert d['gd_onset_year']['value'] == 2002 and d['gd_duration']['value'] == 2
+
+
+def test_label_tile_matches_fused_labels(engine):
+    """lt_label_tile on the fused kernel's own trendline planes gives the same labels."""
+    from land_trendr_amd.engine import label_tile
+    g = golden_io.GoldenScene('lc05')
+    dev = engine.device
+    out = engine.analyze_tile(g.scene, g.params, torch.from_numpy(g.values).to(dev),
+                              torch.from_numpy(g.valid).to(dev))
+    present = (out['winner'] >= 0).to(torch.uint8).contiguous()
+    lab = label_tile(engine, g.scene.years, g.params, out['val_fit'], out['vertex'], present)
+    torch.cuda.synchronize()
+    for f in ('matched', 'onset_year', 'duration'):
+        assert torch.equal(lab[f], out[f]), f
+    a, b = lab['magnitude'].cpu().numpy(), out['magnitude'].cpu().numpy()
+    assert golden_io._bits_equal(a, b).all()

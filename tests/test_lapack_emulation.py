@@ -1,0 +1,98 @@
+"""The device LAPACK emulation (land_trendr_amd/csrc/lt_lapack.h), compiled for the HOST by
+hipcc (tests/native/lapack_host_check.hip), against the oracle's x87 long-double restatement and
+the reference's own lstsq goldens. This runs the kernels' exact arithmetic code without a GPU."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+import golden_io
+from oracle import oracle
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HOSTCHECK = os.path.join(ROOT, 'tests', 'native', 'build', 'liblt_hostcheck.so')
+D = ctypes.POINTER(ctypes.c_double)
+
+
+@pytest.fixture(scope='module')
+def hc():
+    if not os.path.exists(HOSTCHECK):
+        pytest.fail('host harness not built: run __graft_entry__.build()')
+    L = ctypes.CDLL(HOSTCHECK)
+    L.ltx_lstsq.argtypes = [ctypes.c_int, D, D, ctypes.c_int, D]
+    L.ltx_nrm2.argtypes = [ctypes.c_int, D]
+    L.ltx_nrm2.restype = ctypes.c_double
+    return L
+
+
+def _lstsq(hc, x, y, sol=1):
+    x = np.ascontiguousarray(x, np.float64)
+    y = np.ascontiguousarray(y, np.float64)
+    o = (ctypes.c_double * 3)()
+    rc = hc.ltx_lstsq(len(x), x.ctypes.data_as(D), y.ctypes.data_as(D), sol,
+                      ctypes.cast(o, D))
+    return rc, o[0], o[1], o[2]
+
+
+def test_device_lstsq_matches_reference_goldens(hc):
+    z = dict(np.load(os.path.join(golden_io.GOLDEN, 'lstsq.npz')))
+    bad = 0
+    for t in range(len(z['m'])):
+        m = int(z['m'][t])
+        rc, s, c, r = _lstsq(hc, z['x'][t, :m], z['y'][t, :m])
+        assert rc == 0
+        want = (z['slope'][t], z['icpt'][t], z['ssr'][t])
+        bad += not all(golden_io._bits_equal(a, b) for a, b in zip((s, c, r), want))
+    assert bad == 0
+
+
+def test_device_lstsq_matches_oracle_random(hc):
+    rng = np.random.default_rng(2024)
+    bad = 0
+    for t in range(30000):
+        m = int(rng.integers(2, 65))
+        x = np.sort(rng.choice(np.arange(0, 70), m, replace=False)).astype(np.float64)
+        kind = t % 4
+        if kind == 0:
+            y = rng.integers(-3000, 3000, m).astype(np.float64)
+        elif kind == 1:
+            y = rng.normal(0, 1, m) * 10.0 ** rng.integers(-8, 9)
+        elif kind == 2:
+            y = rng.integers(0, 3, m).astype(np.float64)
+        else:
+            y = np.round(rng.normal(0, 40, m)) + np.arange(m) * rng.integers(-60, 60)
+        got = _lstsq(hc, x, y)
+        want = oracle.lstsq(x, y)
+        if got != want and not all(golden_io._bits_equal(a, b) for a, b in zip(got, want)):
+            bad += 1
+        # the DP's residual-only variant must give the same residual
+        r2 = _lstsq(hc, x, y, sol=0)[3]
+        bad += not golden_io._bits_equal(r2, want[3])
+    assert bad == 0
+
+
+def test_soft_float80_nrm2_matches_x87(hc):
+    """dnrm2 over wide-range values: soft-float80 vs the host's x87 long double."""
+    rng = np.random.default_rng(5)
+    lib = oracle.lib()
+    bad = 0
+    for t in range(20000):
+        n = int(rng.integers(1, 70))
+        x = rng.normal(0, 1, n) * 10.0 ** rng.integers(-150, 150, n)
+        x = np.ascontiguousarray(x)
+        got = hc.ltx_nrm2(n, x.ctypes.data_as(D))
+        # oracle: lstsq's H1 uses dnrm2 of x[1:]; compare through the closed form instead
+        ld = np.longdouble(0)
+        acc = [np.longdouble(0)] * 4
+        n8 = n & ~7
+        for j in range(n):
+            v = np.longdouble(x[j])
+            if j < n8:
+                acc[j & 3] = acc[j & 3] + v * v
+            else:
+                acc[0] = acc[0] + v * v
+        tt = ((acc[0] + acc[2]) + acc[1]) + acc[3]
+        want = abs(x[0]) if n == 1 else float(np.sqrt(tt))
+        bad += not golden_io._bits_equal(got, want)
+    assert bad == 0
