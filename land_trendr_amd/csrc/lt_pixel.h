@@ -30,7 +30,7 @@ struct DevScene {
 
 // numpy pairwise sum (n <= 128) of a[0..n-1]: 8 accumulators, then sequential remainder.
 template <class G>
-__device__ inline double np_sum(int n, G a) {
+__host__ __device__ inline double np_sum(int n, G a) {
   if (n < 8) {
     double r = 0.0;
     for (int i = 0; i < n; i++) r += a(i);
@@ -53,7 +53,7 @@ struct RuleState {
   int32_t on[LT_MAX_RULES], du[LT_MAX_RULES];
   double mag[LT_MAX_RULES], init[LT_MAX_RULES];
 
-  __device__ void reset(int nr) {
+  __host__ __device__ void reset(int nr) {
     for (int r = 0; r < nr; r++) {
       have[r] = false;
       on[r] = LT_NODATA;
@@ -65,7 +65,7 @@ struct RuleState {
 
   // One Disturbance (classes.py:170-175) offered to every rule: match_rule's filters
   // (classes.py:190-211) then the FD/GD/LD replacement on strict inequality (:217-230).
-  __device__ void offer(const lt_params& P, int32_t d_on, int32_t d_du, double d_init,
+  __host__ __device__ void offer(const lt_params& P, int32_t d_on, int32_t d_du, double d_init,
                         double d_mag, int& status) {
     for (int r = 0; r < P.n_rules; r++) {
       const lt_rule& R = P.rules[r];
@@ -97,7 +97,7 @@ struct RuleState {
     }
   }
 
-  __device__ void write(const lt_params& P, const lt_tile_out& out, int64_t p) const {
+  __host__ __device__ void write(const lt_params& P, const lt_tile_out& out, int64_t p) const {
     const int64_t os = out.stride;
     for (int r = 0; r < P.n_rules; r++) {
       const int64_t q = (int64_t)r * os + p;
@@ -111,8 +111,80 @@ struct RuleState {
   }
 };
 
+// Screening bound: |LAPACK residual - closed-form residual| <= kScreen * sum(y^2) of the segment.
+// Measured worst case of the emulated dgelsd against the exact rational SSE is 2^-48 * sum(y^2)
+// (tests/test_screening.py), the closed form in double 2^-52: 2^-30 leaves a 2^18 margin.
+constexpr double kScreen = 0x1p-30;
+
+// segmented_least_squares' DP (utils.py:618-631) with candidate screening.
+// For column j every start i is first priced with the closed-form SSE of its segment (exact
+// integer sums for integer data); only the starts whose price lies within the error window of
+// the column minimum are re-priced with the emulated LAPACK residual, and the first exact
+// minimum among them wins — the same argmin and the same OPT bits as pricing every start
+// exactly, because a start outside the window is strictly worse than the approximate argmin.
 template <int MAXY>
-__device__ void analyze_pixel(const DevScene& S, const lt_params& P, const lt_tile_in& in,
+__host__ __device__ inline void dp_screened(int n, const uint8_t* xs, const double* ys, double c,
+                                   double* OPT, uint8_t* arg, int& status) {
+  double va[MAXY];
+  for (int j = 0; j < n; j++) {
+    // pass 1: approximate price of every start, i from j down to 0 (incremental sums)
+    double Sy = 0.0, Sxy = 0.0, Syy = 0.0;
+    int Sx = 0, Sxx = 0;
+    double vmin = __builtin_inf(), wmax = 0.0;
+    for (int i = j; i >= 0; i--) {
+      const int xi = xs[i];
+      const double yi = ys[i];
+      Sx += xi;
+      Sxx += xi * xi;
+      Sy += yi;
+      Sxy += (double)xi * yi;
+      Syy += yi * yi;
+      const int m = j - i + 1;
+      double e = 0.0, w = 0.0;
+      if (m >= 3) {
+        const double md = (double)m;
+        const double D = (double)(m * Sxx - Sx * Sx);
+        const double t1 = md * Syy - Sy * Sy;
+        const double N1 = md * Sxy - (double)Sx * Sy;
+        e = (t1 - N1 * N1 / D) / md;
+        if (e < 0.0) e = 0.0;
+        w = kScreen * Syy;
+      }
+      const double v = (e + c) + OPT[i];
+      w += 0x1p-50 * __builtin_fabs(v);
+      va[i] = v;
+      vmin = v < vmin ? v : vmin;
+      wmax = w > wmax ? w : wmax;
+    }
+    // pass 2: exact price for the starts inside the window, first exact minimum wins
+    const double lim = vmin + 2.0 * wmax;
+    double best = 0.0;
+    int bi = -1;
+    for (int i = 0; i <= j; i++) {
+      if (!(va[i] <= lim)) continue;
+      const int m = j - i + 1;
+      double e = 0.0;
+      if (m >= 3) {
+        double sm, sb, ssr;
+        int rc = lstsq_segment(
+            m, [&](int k) { return (double)xs[i + k]; }, [&](int k) { return ys[i + k]; },
+            false, sm, sb, ssr);
+        if (rc < 0) status |= LT_ST_NUMERIC;
+        e = ssr;
+      }
+      const double v = (e + c) + OPT[i];
+      if (bi < 0 || v < best) {
+        best = v;
+        bi = i;
+      }
+    }
+    OPT[j + 1] = best;
+    arg[j] = (uint8_t)bi;
+  }
+}
+
+template <int MAXY>
+__host__ __device__ void analyze_pixel(const DevScene& S, const lt_params& P, const lt_tile_in& in,
                               const lt_tile_out& out, int64_t p) {
   const int Y = S.n_years;
   const int64_t is = in.stride, os = out.stride;
@@ -206,28 +278,7 @@ __device__ void analyze_pixel(const DevScene& S, const lt_params& P, const lt_ti
     double OPT[MAXY + 1];
     uint8_t arg[MAXY];
     OPT[0] = 0.0;
-    for (int j = 0; j < n; j++) {
-      double best = 0.0;
-      int bi = -1;
-      for (int i = 0; i <= j; i++) {
-        double e = 0.0;
-        if (i != j) {
-          double sm, sb, ssr;
-          int rc = lstsq_segment(
-              j - i + 1, [&](int k) { return (double)xs[i + k]; },
-              [&](int k) { return ys[i + k]; }, false, sm, sb, ssr);
-          if (rc < 0) status |= LT_ST_NUMERIC;
-          e = ssr;
-        }
-        const double v = (e + P.line_cost) + OPT[i];
-        if (bi < 0 || v < best) {
-          best = v;
-          bi = i;
-        }
-      }
-      OPT[j + 1] = best;
-      arg[j] = (uint8_t)bi;
-    }
+    dp_screened<MAXY>(n, xs, ys, P.line_cost, OPT, arg, status);
     // ---- find_segments: starts of the optimal segments + the last point ----
     uint64_t vnon = 1ull << (n - 1);  // over non-spike indices
     for (int j = n - 1; j >= 0; j = arg[j] - 1) vnon |= 1ull << arg[j];
@@ -307,7 +358,7 @@ __device__ void analyze_pixel(const DevScene& S, const lt_params& P, const lt_ti
 
 // Label stage alone (change_labeling on an existing trendline): per slot y, val_fit / vertex /
 // present planes; the first present point is the first left vertex (classes.py:163-164).
-__device__ inline void label_pixel(const int32_t* year, int Y, const lt_params& P,
+__host__ __device__ inline void label_pixel(const int32_t* year, int Y, const lt_params& P,
                                    const lt_label_in& in, const lt_tile_out& out, int64_t p) {
   const int64_t is = in.stride;
   int status = LT_ST_OK;

@@ -1,8 +1,11 @@
-// Host-side harness for the device LAPACK emulation (land_trendr_amd/csrc/lt_lapack.h).
+// Host-side harness for the device code (land_trendr_amd/csrc/lt_lapack.h, lt_pixel.h).
 // TEST INFRASTRUCTURE: compiles the exact __host__ __device__ code the kernels run, for the CPU,
-// so tests/test_lapack_emulation.py can compare it with the oracle (x87 long double) and numpy
-// without a GPU. Built by __graft_entry__.build() into tests/native/build/liblt_hostcheck.so.
-#include "../../land_trendr_amd/csrc/lt_lapack.h"
+// so tests/test_lapack_emulation.py and tests/test_kernel_host.py can compare it with the oracle
+// and the reference goldens without a GPU. Built by __graft_entry__.build() into
+// tests/native/build/liblt_hostcheck.so. Not part of the product (which has no CPU path).
+#include <string.h>
+
+#include "../../land_trendr_amd/csrc/lt_pixel.h"
 
 extern "C" int ltx_lstsq(int m, const double* x, const double* y, int want_solution,
                          double* out3) {
@@ -17,4 +20,27 @@ extern "C" int ltx_lstsq(int m, const double* x, const double* y, int want_solut
 
 extern "C" double ltx_nrm2(int n, const double* x) {
   return lt::nrm2(n, [&](int k) { return x[k]; });
+}
+
+// The kernel's per-pixel pipeline run over a host tile (same structs as lt_analyze_tile).
+extern "C" int ltx_analyze_tile(const lt_scene* sc, const lt_params* prm, const lt_tile_in* in,
+                                const lt_tile_out* out) {
+  static lt::DevScene S;
+  memset(&S, 0, sizeof S);
+  S.n_obs = sc->n_obs;
+  S.n_years = sc->n_years;
+  for (int y = 0; y < sc->n_years; y++) {
+    S.year[y] = sc->year[y];
+    S.feb29_bad[y] = sc->feb29_bad ? sc->feb29_bad[y] : 0;
+  }
+  for (int y = 0; y <= sc->n_years; y++) S.slot_begin[y] = sc->n_years ? sc->slot_begin[y] : 0;
+  for (int k = 0; k < sc->n_obs; k++) {
+    S.order[k] = sc->order[k];
+    S.dist[k] = sc->dist[k];
+  }
+  for (int64_t p = 0; p < in->n_pix; p++) {
+    if (S.n_years <= 32) lt::analyze_pixel<32>(S, *prm, *in, *out, p);
+    else lt::analyze_pixel<64>(S, *prm, *in, *out, p);
+  }
+  return 0;
 }
