@@ -158,6 +158,7 @@ def main():
         dist.barrier()
     stages = eng.stage_ms()
     eng.set_timing(False)
+    n_deferred_last = eng.last_deferred()
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
     if dist is not None:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
@@ -170,6 +171,7 @@ def main():
     value = total_px / elapsed / 1e6
     n_launch = max(1, stages['launches'])
     kern_ms = stages['analyze'] / n_launch
+    resolve_ms = stages['resolve'] / n_launch
     px_per_launch = P * args.steps / n_launch
     flops = f_ref(cfg['years']) * px_per_launch
     achieved = flops / (kern_ms * 1e-3) / 1e12
@@ -193,6 +195,9 @@ def main():
                      'hbm_gbs_algorithmic': round(bytes_per_pixel(cfg, meta.n_obs, meta.n_years)
                                                   * px_per_launch / (kern_ms * 1e-3) / 1e9, 2)},
         'status_numeric_pixels': n_numeric,
+        'resolve_stage': {'ms_per_launch': round(resolve_ms, 3),
+                          'deferred_pixels_last_tile': n_deferred_last,
+                          'last_tile_pixels': tiles[-1][1] - tiles[-1][0]},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res['cpu_baseline'] = cpu_baseline(cfg, args.cpu_seconds)

@@ -140,8 +140,10 @@ int lt_ctx_destroy(lt_ctx* ctx);
 const char* lt_last_error(const lt_ctx* ctx);
 
 /* Full analyze + label of one tile, asynchronous on `stream` (a hipStream_t; NULL = default).
- * Kernels: winner selection (pick_winners) then the fused despike / segmented-least-squares /
- * fit / label kernel. */
+ * Kernels: (1) analyze — winner pick, despike, the lazy segmented-least-squares DP, fits and
+ * labels for every pixel whose optimal path is decided without LAPACK emulation; (2) resolve —
+ * the pixels (1) deferred, with the exact-OPT screened DP. Calls on one context are ordered by
+ * the stream: do not use one context from two streams at once. */
 int lt_analyze_tile(lt_ctx* ctx, const lt_scene* scene, const lt_params* params,
                     const lt_tile_in* in, const lt_tile_out* out, void* stream);
 
@@ -152,9 +154,12 @@ int lt_label_tile(lt_ctx* ctx, const lt_label_in* in, const lt_params* params,
 
 /* Stage timing: when enabled, each lt_analyze_tile brackets its kernels with hipEvents on the
  * launch stream; lt_ctx_stage_ms returns the accumulated milliseconds per stage
- * (0 = winner selection, 1 = analyze/label) since the last reset and the launch count. */
+ * (0 = analyze: every pixel with the lazy DP, 1 = resolve: the deferred pixels with the exact-OPT
+ * DP) since the last call, and the number of lt_analyze_tile calls. */
 int lt_ctx_set_timing(lt_ctx* ctx, int enable);
 int lt_ctx_stage_ms(lt_ctx* ctx, double* ms_out, int n_stages, int64_t* n_launches);
+/* Pixels the last lt_analyze_tile deferred to the resolve stage (synchronous read). */
+int lt_ctx_last_deferred(lt_ctx* ctx, int64_t* n_deferred);
 
 #ifdef __cplusplus
 }

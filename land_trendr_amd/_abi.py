@@ -78,7 +78,8 @@ PIX_FIELDS = [('status', 'int32'), ('n_years', 'int32')]
 
 # symbols include/lt_abi.h declares (checked by tests/test_abi.py)
 EXPORTS = ['lt_abi_version', 'lt_ctx_create', 'lt_ctx_destroy', 'lt_last_error',
-           'lt_analyze_tile', 'lt_label_tile', 'lt_ctx_set_timing', 'lt_ctx_stage_ms']
+           'lt_analyze_tile', 'lt_label_tile', 'lt_ctx_set_timing', 'lt_ctx_stage_ms',
+           'lt_ctx_last_deferred']
 
 _LIB = None
 
@@ -105,6 +106,7 @@ def load_lib(path=None):
                                   ctypes.POINTER(LtTileOut), vp]
     lib.lt_ctx_set_timing.argtypes = [vp, ctypes.c_int]
     lib.lt_ctx_stage_ms.argtypes = [vp, c_f64p, ctypes.c_int, ctypes.POINTER(ctypes.c_int64)]
+    lib.lt_ctx_last_deferred.argtypes = [vp, ctypes.POINTER(ctypes.c_int64)]
     if lib.lt_abi_version() != LT_ABI_VERSION:
         raise RuntimeError('liblt_hip.so ABI %d != %d' % (lib.lt_abi_version(), LT_ABI_VERSION))
     if path is None:

@@ -11,19 +11,66 @@
 #include <vector>
 
 #include "../../include/lt_abi.h"
+#include "lt_fast.h"
 #include "lt_pixel.h"
 
 namespace {
 
 constexpr int kBlock = 256;
 
+// Stage 1: every pixel with the lazy DP. Pixels whose optimal path crosses an ambiguous column
+// are appended (wave-aggregated) to `defer` for the resolve stage.
 template <int MAXY>
 __global__ __launch_bounds__(kBlock) void analyze_kernel(const lt::DevScene* __restrict__ S,
                                                          const lt_params P, const lt_tile_in in,
-                                                         const lt_tile_out out) {
+                                                         const lt_tile_out out,
+                                                         int64_t* __restrict__ defer,
+                                                         unsigned long long* __restrict__ n_defer) {
   const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (p >= in.n_pix) return;
-  lt::analyze_pixel<MAXY>(*S, P, in, out, p);
+  const bool deferred = !lt::analyze_pixel<MAXY, true>(*S, P, in, out, p);
+  const uint64_t mask = __ballot(deferred);
+  if (mask == 0) return;
+  const int lane = threadIdx.x & 63;
+  const int leader = __ffsll((long long)mask) - 1;
+  unsigned long long base = 0;
+  if (lane == leader) base = atomicAdd(n_defer, (unsigned long long)__popcll(mask));
+  base = __shfl(base, leader);
+  if (deferred) defer[base + __popcll(mask & ((1ull << lane) - 1))] = p;
+}
+
+// Stage 1 (wave-lockstep body, lt_fast.h): one wave per workgroup, the pixel series in LDS.
+template <int MAXY>
+__global__ __launch_bounds__(64) void analyze_fast_kernel(const lt::DevScene* __restrict__ S,
+                                                          const lt_params P, const lt_tile_in in,
+                                                          const lt_tile_out out,
+                                                          int64_t* __restrict__ defer,
+                                                          unsigned long long* __restrict__ n_defer) {
+  __shared__ lt::WaveLds<MAXY> L;
+  const int lane = threadIdx.x;
+  const int64_t p = (int64_t)blockIdx.x * 64 + lane;
+  const bool live = p < in.n_pix;
+  const bool deferred = !lt::analyze_fast<MAXY>(*S, P, in, out, p, live, lane, L) && live;
+  const uint64_t mask = __ballot(deferred);
+  if (mask == 0) return;
+  const int leader = __ffsll((long long)mask) - 1;
+  unsigned long long base = 0;
+  if (lane == leader) base = atomicAdd(n_defer, (unsigned long long)__popcll(mask));
+  base = __shfl(base, leader);
+  if (deferred) defer[base + __popcll(mask & ((1ull << lane) - 1))] = p;
+}
+
+// Stage 2: the deferred pixels with the exact-OPT screened DP (grid-stride over the list).
+template <int MAXY>
+__global__ __launch_bounds__(kBlock) void resolve_kernel(const lt::DevScene* __restrict__ S,
+                                                         const lt_params P, const lt_tile_in in,
+                                                         const lt_tile_out out,
+                                                         const int64_t* __restrict__ defer,
+                                                         const unsigned long long* __restrict__ n_defer) {
+  const int64_t n = (int64_t)*n_defer;
+  for (int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x; k < n;
+       k += (int64_t)gridDim.x * kBlock)
+    lt::analyze_pixel<MAXY, false>(*S, P, in, out, defer[k]);
 }
 
 struct YearArg {
@@ -52,10 +99,12 @@ struct lt_ctx {
   hipEvent_t scene_copied = nullptr;
   bool scene_valid = false;
   bool timing = false;
-  std::vector<EventPair> pool;   // all events ever created (reused)
+  std::vector<EventPair> pool;   // all events ever created (reused): 2 pairs per launch
   size_t used = 0;               // pairs recorded since the last stage_ms call
-  double acc_ms = 0.0;
   int64_t launches = 0;
+  int64_t* d_defer = nullptr;    // deferred-pixel list of the resolve stage
+  unsigned long long* d_ndefer = nullptr;
+  int64_t defer_cap = 0;
 };
 
 static int fail(lt_ctx* c, int code, const char* fmt, const char* detail = "") {
@@ -106,6 +155,8 @@ int lt_ctx_destroy(lt_ctx* c) {
     (void)hipEventDestroy(ep.start);
     (void)hipEventDestroy(ep.stop);
   }
+  if (c->d_defer) (void)hipFree(c->d_defer);
+  if (c->d_ndefer) (void)hipFree(c->d_ndefer);
   if (c->d_scene) (void)hipFree(c->d_scene);
   if (c->h_scene) (void)hipHostFree(c->h_scene);
   delete c;
@@ -123,19 +174,16 @@ int lt_ctx_set_timing(lt_ctx* c, int enable) {
 int lt_ctx_stage_ms(lt_ctx* c, double* ms_out, int n_stages, int64_t* n_launches) {
   if (!c) return LT_ERR_ARG;
   HIP_OR_FAIL(c, hipSetDevice(c->device));
-  double acc = c->acc_ms;
+  double acc[2] = {0.0, 0.0};
   for (size_t i = 0; i < c->used; i++) {
     HIP_OR_FAIL(c, hipEventSynchronize(c->pool[i].stop));
     float ms = 0.f;
     HIP_OR_FAIL(c, hipEventElapsedTime(&ms, c->pool[i].start, c->pool[i].stop));
-    acc += ms;
+    acc[i & 1] += ms;  // pairs alternate: analyze stage, resolve stage
   }
-  for (int s = 0; s < n_stages; s++) ms_out[s] = 0.0;
-  if (n_stages > 1) ms_out[1] = acc;  // stage 1: fused winner+analyze+label kernel
-  else if (n_stages == 1) ms_out[0] = acc;
+  for (int s = 0; s < n_stages; s++) ms_out[s] = s < 2 ? acc[s] : 0.0;
   if (n_launches) *n_launches = c->launches;
   c->used = 0;
-  c->acc_ms = 0.0;
   c->launches = 0;
   return LT_OK;
 }
@@ -196,27 +244,68 @@ int lt_analyze_tile(lt_ctx* c, const lt_scene* sc, const lt_params* prm, const l
     c->scene_valid = true;
   }
 
-  EventPair* ep = nullptr;
+  // deferred-pixel list (grown on demand; sized for the largest tile seen)
+  if (c->defer_cap < in->n_pix) {
+    if (c->d_defer) HIP_OR_FAIL(c, hipFree(c->d_defer));
+    c->d_defer = nullptr;
+    HIP_OR_FAIL(c, hipMalloc((void**)&c->d_defer, sizeof(int64_t) * (size_t)in->n_pix));
+    if (!c->d_ndefer) HIP_OR_FAIL(c, hipMalloc((void**)&c->d_ndefer, sizeof(unsigned long long)));
+    c->defer_cap = in->n_pix;
+  }
+  HIP_OR_FAIL(c, hipMemsetAsync(c->d_ndefer, 0, sizeof(unsigned long long), stream));
+
+  EventPair* ep[2] = {nullptr, nullptr};
   if (c->timing) {
-    if (c->used == c->pool.size()) {
+    while (c->pool.size() < c->used + 2) {  // grow first: pointers into the pool stay valid
       EventPair np;
       HIP_OR_FAIL(c, hipEventCreate(&np.start));
       HIP_OR_FAIL(c, hipEventCreate(&np.stop));
       c->pool.push_back(np);
     }
-    ep = &c->pool[c->used++];
-    HIP_OR_FAIL(c, hipEventRecord(ep->start, stream));
+    ep[0] = &c->pool[c->used++];
+    ep[1] = &c->pool[c->used++];
   }
   const int64_t nblk = (in->n_pix + kBlock - 1) / kBlock;
   if (nblk > 0x7fffffff) return fail(c, LT_ERR_LIMIT, "tile too large%s");
   dim3 grid((unsigned)nblk), block(kBlock);
+  // resolve stage: a fixed grid striding over however many pixels were deferred
+  dim3 rgrid((unsigned)(nblk < 2048 ? nblk : 2048));
+  if (ep[0]) HIP_OR_FAIL(c, hipEventRecord(ep[0]->start, stream));
+  const int64_t nwave = (in->n_pix + 63) / 64;
+  if (nwave > 0x7fffffff) return fail(c, LT_ERR_LIMIT, "tile too large%s");
+  dim3 fgrid((unsigned)nwave), fblock(64);
   if (Y <= 32)
-    hipLaunchKernelGGL(analyze_kernel<32>, grid, block, 0, stream, c->d_scene, *prm, *in, *out);
+    hipLaunchKernelGGL(analyze_fast_kernel<32>, fgrid, fblock, 0, stream, c->d_scene, *prm, *in,
+                       *out, c->d_defer, c->d_ndefer);
+  else if (Y <= 48)
+    hipLaunchKernelGGL(analyze_fast_kernel<48>, fgrid, fblock, 0, stream, c->d_scene, *prm, *in,
+                       *out, c->d_defer, c->d_ndefer);
   else
-    hipLaunchKernelGGL(analyze_kernel<64>, grid, block, 0, stream, c->d_scene, *prm, *in, *out);
+    hipLaunchKernelGGL(analyze_fast_kernel<64>, fgrid, fblock, 0, stream, c->d_scene, *prm, *in,
+                       *out, c->d_defer, c->d_ndefer);
   HIP_OR_FAIL(c, hipGetLastError());
-  if (ep) HIP_OR_FAIL(c, hipEventRecord(ep->stop, stream));
+  if (ep[0]) HIP_OR_FAIL(c, hipEventRecord(ep[0]->stop, stream));
+  if (ep[1]) HIP_OR_FAIL(c, hipEventRecord(ep[1]->start, stream));
+  if (Y <= 32)
+    hipLaunchKernelGGL(resolve_kernel<32>, rgrid, block, 0, stream, c->d_scene, *prm, *in, *out,
+                       c->d_defer, c->d_ndefer);
+  else
+    hipLaunchKernelGGL(resolve_kernel<64>, rgrid, block, 0, stream, c->d_scene, *prm, *in, *out,
+                       c->d_defer, c->d_ndefer);
+  HIP_OR_FAIL(c, hipGetLastError());
+  if (ep[1]) HIP_OR_FAIL(c, hipEventRecord(ep[1]->stop, stream));
   c->launches++;
+  return LT_OK;
+}
+
+int lt_ctx_last_deferred(lt_ctx* c, int64_t* n_deferred) {
+  if (!c || !n_deferred) return LT_ERR_ARG;
+  *n_deferred = 0;
+  if (!c->d_ndefer) return LT_OK;
+  HIP_OR_FAIL(c, hipSetDevice(c->device));
+  unsigned long long v = 0;
+  HIP_OR_FAIL(c, hipMemcpy(&v, c->d_ndefer, sizeof v, hipMemcpyDeviceToHost));
+  *n_deferred = (int64_t)v;
   return LT_OK;
 }
 

@@ -1,0 +1,367 @@
+// lt_fast.h — the analyze stage as a wave-lockstep kernel body (one pixel per lane, one wave per
+// workgroup). Same results as analyze_pixel<.., true> in lt_pixel.h, organised for CDNA4:
+//
+//   * per-lane series live in LDS as [index][lane] planes: lane l of element k is at
+//     base + (k*64 + l) * sizeof(T), so any per-lane index k is bank-conflict free
+//     (ds_read_b64: bank = (2l) mod 64 within each 32-lane group);
+//   * loops run over a wave-uniform counter (series position, DP column, vertex number, rule)
+//     with per-lane predicates, so the expensive calls (LAPACK-emulated vertex fits) are issued
+//     once per vertex NUMBER for the whole wave instead of once per series position per lane;
+//   * the DP keeps OPT in registers (static indices from the unrolled inner loop) and decides a
+//     column without LAPACK emulation whenever the closed-form prices separate (dp_lazy's rule);
+//   * no scratch memory.
+#pragma once
+#include "lt_pixel.h"
+
+namespace lt {
+
+// max over the 64 lanes of a wave (every lane must call it)
+__device__ inline int wave_max(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const int u = __shfl_xor(v, o);
+    v = u > v ? u : v;
+  }
+  return v;
+}
+
+template <int MAXY>
+struct WaveLds {
+  double ys[MAXY][64];   // present values (t), compacted in place to non-spike (k); later vertex fits
+  uint8_t xc[MAXY][64];  // year offset of present point t
+  uint8_t sc[MAXY][64];  // scene slot of present point t
+  uint8_t xn[MAXY][64];  // year offset of non-spike point k
+  uint8_t tk[MAXY][64];  // present index t of non-spike point k
+  uint8_t ag[MAXY][64];  // DP argmin of column k
+  uint8_t vt[MAXY][64];  // non-spike index of vertex q
+};
+
+// Returns false when the pixel's optimal path crosses an ambiguous DP column (resolve stage).
+template <int MAXY>
+__device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const lt_tile_in& in,
+                                   const lt_tile_out& out, int64_t p, bool live, int lane,
+                                   WaveLds<MAXY>& L) {
+  const int Y = S.n_years;
+  const int64_t is = in.stride, os = out.stride;
+  const double nan = __builtin_nan("");
+  int status = LT_ST_OK;
+
+  // ---- pick_winners (utils.py:491-521) over wave-uniform year slots ----
+  int T = 0, y0 = 0;
+  for (int y = 0; y < Y; y++) {
+    int best = -1, bd = 0x7fffffff;
+    const int k1 = S.slot_begin[y + 1];
+    for (int k = S.slot_begin[y]; k < k1; k++) {
+      const int o = S.order[k];
+      const bool ok = live && (in.obs_valid == nullptr || in.obs_valid[(int64_t)o * is + p] != 0);
+      if (ok && S.dist[k] < bd) {
+        bd = S.dist[k];
+        best = o;
+      }
+    }
+    if (!live) continue;
+    const int64_t q = (int64_t)y * os + p;
+    if (out.winner) out.winner[q] = (int16_t)best;
+    if (best >= 0) {
+      if (S.feb29_bad[y]) status |= LT_ST_FEB29;
+      const double v = in.obs_val[(int64_t)best * is + p];
+      if (T == 0) y0 = S.year[y];
+      L.ys[T][lane] = v;
+      L.xc[T][lane] = (uint8_t)(S.year[y] - y0);
+      L.sc[T][lane] = (uint8_t)y;
+      T++;
+      if (out.val_raw) out.val_raw[q] = v;
+    } else {
+      if (out.val_raw) out.val_raw[q] = nan;
+      if (out.val_fit) out.val_fit[q] = nan;
+      if (out.fit_m) out.fit_m[q] = nan;
+      if (out.fit_b) out.fit_b[q] = nan;
+      if (out.right_m) out.right_m[q] = nan;
+      if (out.right_b) out.right_b[q] = nan;
+      if (out.spike) out.spike[q] = 0;
+      if (out.vertex) out.vertex[q] = 0;
+    }
+  }
+  const bool ok = live && T >= 2;
+  if (live && T == 0) status |= LT_ST_EMPTY;
+  if (live && T == 1) status |= LT_ST_SINGLE_YEAR;
+  const int Tmax = wave_max(ok ? T : 0);
+
+  // ---- despike (utils.py:556-582): numpy pairwise std, then the 3-window scan ----
+  uint64_t spike = 0;
+  int n = 0;
+  if (Tmax >= 2) {
+    const int n8 = ok ? T - (T % 8) : 0;
+    // np.sum: 8 accumulators over the first n - n%8 elements (n >= 8), else sequential
+    auto npsum = [&](auto term) {
+      double r0 = 0.0, r1 = 0.0, r2 = 0.0, r3 = 0.0, r4 = 0.0, r5 = 0.0, r6 = 0.0, r7 = 0.0;
+      double seq = 0.0;
+      for (int t = 0; t < Tmax; t++) {
+        if (!(ok && t < T)) continue;
+        const double a = term(t);
+        if (T < 8) {
+          seq += a;
+        } else if (t < n8) {
+          switch (t & 7) {
+            case 0: r0 = t < 8 ? a : r0 + a; break;
+            case 1: r1 = t < 8 ? a : r1 + a; break;
+            case 2: r2 = t < 8 ? a : r2 + a; break;
+            case 3: r3 = t < 8 ? a : r3 + a; break;
+            case 4: r4 = t < 8 ? a : r4 + a; break;
+            case 5: r5 = t < 8 ? a : r5 + a; break;
+            case 6: r6 = t < 8 ? a : r6 + a; break;
+            default: r7 = t < 8 ? a : r7 + a; break;
+          }
+          if (t == n8 - 1) seq = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+        } else {
+          seq += a;
+        }
+      }
+      return seq;
+    };
+    const double avg = npsum([&](int t) { return L.ys[t][lane]; }) / (double)T;
+    const double sd = __builtin_sqrt(npsum([&](int t) {
+                                       const double d = avg - L.ys[t][lane];
+                                       return d * d;
+                                     }) /
+                                     (double)T);
+    double last_good = ok ? L.ys[0][lane] : 0.0;
+    double xv = last_good, yv = ok ? L.ys[1][lane] : 0.0;
+    for (int t = 1; t + 1 < Tmax; t++) {
+      if (!(ok && t + 1 < T)) continue;
+      const double zv = L.ys[t + 1][lane];
+      const bool mono = (xv <= yv && yv <= zv) || (xv >= yv && yv >= zv);
+      if (!mono && (__builtin_fabs(yv - xv) > sd && __builtin_fabs(yv - zv) > sd) &&
+          yv != last_good) {
+        spike |= 1ull << t;
+      } else {
+        last_good = yv;
+      }
+      xv = yv;
+      yv = zv;
+    }
+    // dropna: compact the non-spike points in place (k <= t)
+    for (int t = 0; t < Tmax; t++) {
+      if (!(ok && t < T) || ((spike >> t) & 1)) continue;
+      L.ys[n][lane] = L.ys[t][lane];
+      L.xn[n][lane] = L.xc[t][lane];
+      L.tk[n][lane] = (uint8_t)t;
+      n++;
+    }
+  }
+  const int nmax = wave_max(n);
+
+  // ---- segmented least squares DP (utils.py:618-631), decided lazily ----
+  bool deferred = false;
+  uint64_t vmask = 0;  // vertices over non-spike indices
+  if (nmax >= 1) {
+    const double c = P.line_cost;
+    const double inf = __builtin_inf();
+    double OPTa[MAXY + 1];
+#pragma unroll
+    for (int k = 0; k <= MAXY; k++) OPTa[k] = 0.0;
+    uint64_t exact = 1;      // bit k: OPTa[k] is the reference value itself
+    double Emax = 0.0;       // bound on |OPTa[k] - OPT[k]| for every inexact k so far
+    int pv_cur = 0, pv_prev = 0;  // provenance of OPTa[j] and OPTa[j-1]
+    uint64_t amb = 0;
+    for (int j = 0; j < nmax; j++) {
+      const bool col = j < n;
+      double Sy = 0.0, Sxy = 0.0, Syy = 0.0;
+      int Sx = 0, Sxx = 0;
+      double Ve = inf, Hi = inf, Li1 = inf, Li2 = inf, vHi = 0.0, wHi = 0.0, vbest = inf;
+      int ie = 0, iHi = 0, ibest = 0, keyHi = -1, keyL1 = -2;
+#pragma unroll
+      for (int i = MAXY - 1; i >= 0; i--) {
+        if (i > j) continue;  // wave-uniform
+        const int xi = L.xn[i][lane];
+        const double yi = L.ys[i][lane];
+        Sx += xi;
+        Sxx += xi * xi;
+        Sy += yi;
+        Sxy += (double)xi * yi;
+        Syy += yi * yi;
+        const int m = j - i + 1;
+        const bool ex_i = (exact >> i) & 1;
+        double e = 0.0, w = ex_i ? 0.0 : Emax;
+        if (m >= 3) {
+          const double md = (double)m;
+          const double D = (double)(m * Sxx - Sx * Sx);
+          const double t1 = md * Syy - Sy * Sy;
+          const double N1 = md * Sxy - (double)Sx * Sy;
+          e = (t1 - N1 * N1 / D) / md;
+          e = e < 0.0 ? 0.0 : e;
+          w += kScreen * Syy;
+        }
+        const double v = (e + c) + OPTa[i];
+        if (v <= vbest) {
+          vbest = v;
+          ibest = i;
+        }
+        if (w == 0.0) {
+          if (v <= Ve) {
+            Ve = v;
+            ie = i;
+          }
+          continue;
+        }
+        w += 0x1p-50 * __builtin_fabs(v);
+        const int key = m >= 3 ? 0x10000 | i : (m == 1 ? pv_cur : pv_prev) + 1;
+        const double lo = v - w, hi = v + w;
+        if (hi <= Hi) {
+          Hi = hi;
+          iHi = i;
+          keyHi = key;
+          vHi = v;
+          wHi = w;
+        }
+        if (lo <= Li1) {
+          if (key != keyL1) Li2 = Li1;
+          Li1 = lo;
+          keyL1 = key;
+        } else if (lo < Li2 && key != keyL1) {
+          Li2 = lo;
+        }
+      }
+      const double H = Hi < Ve ? Hi : Ve;
+      int a;
+      double vnew, enew = 0.0;
+      int pnew = 0;
+      bool exnew = false;
+      if (Li1 > H) {
+        a = ie;
+        vnew = Ve;
+        exnew = true;
+      } else if (keyL1 == keyHi && Li2 > H && Ve > H) {
+        a = iHi;
+        vnew = vHi;
+        enew = wHi;
+        pnew = keyHi >= 0x10000 ? (j + 1) << 8 : keyHi;
+      } else {
+        if (col) amb |= 1ull << j;
+        a = ibest;
+        vnew = vbest;
+        const double Lo = Li1 < Ve ? Li1 : Ve;
+        enew = (H - Lo) * (1.0 + 0x1p-40) + 0x1p-50 * __builtin_fabs(vbest);
+        pnew = (j + 1) << 8;
+      }
+      if (col) {
+        L.ag[j][lane] = (uint8_t)a;
+#pragma unroll
+        for (int k = 1; k <= MAXY; k++)
+          if (k == j + 1) OPTa[k] = vnew;  // wave-uniform index
+        if (exnew) exact |= 2ull << j;
+        Emax = enew > Emax ? enew : Emax;
+        pv_prev = pv_cur;
+        pv_cur = pnew;
+      }
+    }
+    // find_segments (utils.py:633-644): starts of the optimal segments + the last point
+    if (n >= 1) {
+      vmask = 1ull << (n - 1);
+      for (int j = n - 1; j >= 0;) {
+        const int a = L.ag[j][lane];
+        if ((amb >> j) & 1) deferred = true;
+        vmask |= 1ull << a;
+        j = a - 1;
+      }
+    }
+  }
+  if (deferred) return false;
+
+  // ---- vertices2eqns + eqns2fitted_points in lockstep over the vertex number q ----
+  int nv = 0;
+  for (uint64_t m = vmask; m; m &= m - 1) L.vt[nv++][lane] = (uint8_t)__builtin_ctzll(m);
+  const int nvmax = wave_max(nv);
+  double pm = 0.0, pb = 0.0;   // eqn of vertex q-1
+  for (int q = 0; q < nvmax; q++) {
+    const bool act = q < nv;
+    const int ka = act ? L.vt[q][lane] : 0;
+    const bool has_next = act && q + 1 < nv;
+    const int kb = has_next ? L.vt[q + 1][lane] : ka;
+    double cm = pm, cb = pb;
+    // one LAPACK-emulated fit per vertex number for the whole wave (lanes without a next
+    // vertex reuse the previous equation, utils.py:662)
+    const int mseg = has_next ? kb - ka + 1 : 2;
+    const int kbase = has_next ? ka : 0;
+    double sm = 0.0, sbv = 0.0, ssr = 0.0;
+    if (__ballot(has_next)) {
+      const int rc = lstsq_segment(
+          mseg, [&](int k) { return has_next ? (double)L.xn[kbase + k][lane] : (double)k; },
+          [&](int k) { return has_next ? L.ys[kbase + k][lane] : 0.0; }, true, sm, sbv, ssr);
+      if (has_next) {
+        if (rc < 0) status |= LT_ST_NUMERIC;
+        cm = sm;
+        cb = sbv;
+      }
+    }
+    // emit the vertex point and the points up to the next vertex (spikes included)
+    const int ta = act ? L.tk[ka][lane] : 0;
+    const int tb = has_next ? L.tk[kb][lane] : ta + 1;
+    const int span = act ? tb - ta : 0;
+    const int spanmax = wave_max(span);
+    const double raw_v = act ? L.ys[ka][lane] : 0.0;
+    double fit_vertex = 0.0;
+    for (int s = 0; s < spanmax; s++) {
+      if (s >= span) continue;
+      const int t = ta + s;
+      const double x = (double)L.xc[t][lane];
+      double fv, fmv, fbv;
+      if (s == 0 && q > 0 && !(pm == cm && pb == cb)) {
+        const double fl = (pm * x) + pb;
+        const double fr = (cm * x) + cb;
+        if (__builtin_fabs(fl - raw_v) <= __builtin_fabs(fr - raw_v)) {
+          fv = fl; fmv = pm; fbv = pb;
+        } else {
+          fv = fr; fmv = cm; fbv = cb;
+        }
+      } else {
+        fv = (cm * x) + cb;
+        fmv = cm;
+        fbv = cb;
+      }
+      if (s == 0) fit_vertex = fv;
+      const int64_t o = (int64_t)L.sc[t][lane] * os + p;
+      if (out.val_fit) out.val_fit[o] = fv;
+      if (out.fit_m) out.fit_m[o] = fmv;
+      if (out.fit_b) out.fit_b[o] = fbv;
+      if (out.right_m) out.right_m[o] = cm;
+      if (out.right_b) out.right_b[o] = cb;
+      if (out.spike) out.spike[o] = (uint8_t)((spike >> t) & 1);
+      if (out.vertex) out.vertex[o] = s == 0 ? 1 : 0;
+    }
+    if (act) L.ys[q][lane] = fit_vertex;  // q <= ka: the raw values still needed sit above q
+    pm = cm;
+    pb = cb;
+  }
+
+  // ---- change_labeling (utils.py:795-820): rules outer, disturbances inner ----
+  for (int r = 0; r < P.n_rules; r++) {
+    RuleState1 rs;
+    for (int q = 1; q < nvmax; q++) {
+      if (q >= nv) continue;
+      const int32_t on = y0 + L.xn[L.vt[q - 1][lane]][lane];
+      const int32_t yr = y0 + L.xn[L.vt[q][lane]][lane];
+      const double f0 = L.ys[q - 1][lane], f1 = L.ys[q][lane];
+      rs.offer(P.rules[r], P.pre_threshold_mode, on, yr - on, f0, f0 - f1, status);
+    }
+    if (live) rs.write(P.rules[r], out, (int64_t)r * os + p);
+  }
+  if (!live) return true;
+  if (!ok) {  // the reference raises for this pixel: per-year fields of present years are NaN
+    for (int t = 0; t < T; t++) {
+      const int64_t o = (int64_t)L.sc[t][lane] * os + p;
+      if (out.val_fit) out.val_fit[o] = nan;
+      if (out.fit_m) out.fit_m[o] = nan;
+      if (out.fit_b) out.fit_b[o] = nan;
+      if (out.right_m) out.right_m[o] = nan;
+      if (out.right_b) out.right_b[o] = nan;
+      if (out.spike) out.spike[o] = 0;
+      if (out.vertex) out.vertex[o] = 0;
+    }
+  }
+  if (out.n_years) out.n_years[p] = T;
+  if (out.status) out.status[p] = status;
+  return true;
+}
+
+}  // namespace lt

@@ -47,6 +47,52 @@ __host__ __device__ inline double np_sum(int n, G a) {
   return res;
 }
 
+// change_labeling state of ONE rule: match_rule's filters (classes.py:190-211) and the FD/GD/LD
+// winner replacement on strict inequality (classes.py:217-230).
+struct RuleState1 {
+  bool have = false;
+  int32_t on = LT_NODATA, du = LT_NODATA;
+  double mag = (double)LT_NODATA, init = (double)LT_NODATA;
+
+  __host__ __device__ void offer(const lt_rule& R, int pre_mode, int32_t d_on, int32_t d_du,
+                                 double d_init, double d_mag, int& status) {
+    bool match = true;
+    if (R.onset_op == LT_Q_EQ) match = match && ((double)d_on == R.onset_val);
+    else if (R.onset_op == LT_Q_LE) match = match && !((double)d_on > R.onset_val);
+    else if (R.onset_op == LT_Q_GE) match = match && !((double)d_on < R.onset_val);
+    if (R.duration_op == LT_Q_GT) match = match && !((double)d_du <= R.duration_val);
+    else if (R.duration_op == LT_Q_LT) match = match && !((double)d_du >= R.duration_val);
+    if (R.pre_op != LT_Q_UNSET) {
+      if (pre_mode == LT_PRE_REFERENCE) status |= LT_ST_PRE_THRESHOLD_ATTR;
+      else if (R.pre_op == LT_Q_GT) match = match && !(d_init <= R.pre_val);
+      else if (R.pre_op == LT_Q_LT) match = match && !(d_init >= R.pre_val);
+    }
+    if (!match) return;
+    bool take = !have;
+    if (have) {
+      if (R.change_type == LT_CT_FD) take = d_on < on;
+      else if (R.change_type == LT_CT_GD) take = d_mag > mag;
+      else if (R.change_type == LT_CT_LD) take = d_du > du;
+    }
+    if (take) {
+      have = true;
+      on = d_on;
+      du = d_du;
+      mag = d_mag;
+      init = d_init;
+    }
+  }
+
+  __host__ __device__ void write(const lt_rule& R, const lt_tile_out& out, int64_t q) const {
+    if (out.matched) out.matched[q] = have ? 1 : 0;
+    if (out.class_val) out.class_val[q] = have ? R.class_val : LT_NODATA;
+    if (out.onset_year) out.onset_year[q] = on;
+    if (out.duration) out.duration[q] = du;
+    if (out.magnitude) out.magnitude[q] = mag;
+    if (out.initial_val) out.initial_val[q] = init;
+  }
+};
+
 // change_labeling state for all rules (classes.py:213-230 winner bookkeeping).
 struct RuleState {
   bool have[LT_MAX_RULES];
@@ -183,9 +229,116 @@ __host__ __device__ inline void dp_screened(int n, const uint8_t* xs, const doub
   }
 }
 
+// The same DP with every OPT value kept only approximately, together with a rigorous bound
+// E[j] >= |OPTa[j] - OPT[j]|. Column j is decided without any LAPACK emulation when one start's
+// upper bound lies strictly below every other start's lower bound (then it is the unique exact
+// minimum). Otherwise the column is marked ambiguous, carries the approximate minimum and the
+// width of the uncertainty forward, and the DP goes on. Only the backtracked path matters for
+// the result: if it crosses no ambiguous column, every vertex is exact; otherwise the function
+// returns false and the pixel is re-run with dp_screened (exact OPT) by the resolve kernel.
 template <int MAXY>
-__host__ __device__ void analyze_pixel(const DevScene& S, const lt_params& P, const lt_tile_in& in,
-                              const lt_tile_out& out, int64_t p) {
+__host__ __device__ inline bool dp_lazy(int n, const uint8_t* xs, const double* ys, double c,
+                                        uint8_t* arg, uint64_t* amb_out = nullptr) {
+  // prov[k]: provenance of an inexact OPTa[k] = (base column << 8 | depth): the value is the
+  // base column's value with `depth` further "(0 + c) + ." steps applied. Equal provenance means
+  // the same operations on the same operand, i.e. bitwise-equal reference values.
+  double OPTa[MAXY + 1], E[MAXY + 1];
+  uint16_t prov[MAXY + 1];
+  uint64_t amb = 0;
+  OPTa[0] = 0.0;
+  E[0] = 0.0;
+  prov[0] = 0;
+  for (int j = 0; j < n; j++) {
+    double Sy = 0.0, Sxy = 0.0, Syy = 0.0;
+    int Sx = 0, Sxx = 0;
+    // Exact candidates (1-2 point segment: residual exactly 0, on an exact OPT) are computed
+    // with the reference's own operations, so their value IS the reference's; the others carry
+    // an interval [v - w, v + w] around the reference value.
+    const double inf = __builtin_inf();
+    double Ve = inf;                   // min exact value; ie = first start attaining it
+    double Hi = inf, Li1 = inf, Li2 = inf, vHi = 0.0, wHi = 0.0, vbest = inf;
+    int ie = -1, iHi = -1, ibest = -1;
+    int keyHi = -1, keyL1 = -2;
+    for (int i = j; i >= 0; i--) {
+      const int xi = xs[i];
+      const double yi = ys[i];
+      Sx += xi;
+      Sxx += xi * xi;
+      Sy += yi;
+      Sxy += (double)xi * yi;
+      Syy += yi * yi;
+      const int m = j - i + 1;
+      double e = 0.0, w = E[i];
+      if (m >= 3) {
+        const double md = (double)m;
+        const double D = (double)(m * Sxx - Sx * Sx);
+        const double t1 = md * Syy - Sy * Sy;
+        const double N1 = md * Sxy - (double)Sx * Sy;
+        e = (t1 - N1 * N1 / D) / md;
+        if (e < 0.0) e = 0.0;
+        w += kScreen * Syy;
+      }
+      const double v = (e + c) + OPTa[i];
+      if (v <= vbest) {  // i descends: "<=" keeps the smaller start on equal values
+        vbest = v;
+        ibest = i;
+      }
+      if (w == 0.0) {
+        if (v <= Ve) {
+          Ve = v;
+          ie = i;
+        }
+        continue;
+      }
+      w += 0x1p-50 * __builtin_fabs(v);
+      // candidates with equal keys have bitwise-equal reference values (and equal v, w)
+      const int key = m >= 3 ? 0x10000 | i : (int)prov[i] + 1;
+      const double lo = v - w, hi = v + w;
+      if (hi <= Hi) {
+        Hi = hi;
+        iHi = i;
+        keyHi = key;
+        vHi = v;
+        wHi = w;
+      }
+      if (lo <= Li1) {
+        if (key != keyL1) Li2 = Li1;
+        Li1 = lo;
+        keyL1 = key;
+      } else if (lo < Li2 && key != keyL1) {
+        Li2 = lo;
+      }
+    }
+    const double H = Hi < Ve ? Hi : Ve;  // the exact minimum lies in [min lower bound, H]
+    if (Li1 > H) {  // no interval reaches H: the exact candidates decide, bit-exactly
+      arg[j] = (uint8_t)ie;
+      OPTa[j + 1] = Ve;
+      E[j + 1] = 0.0;
+      prov[j + 1] = 0;
+    } else if (keyL1 == keyHi && Li2 > H && Ve > H) {  // one value lies below all others
+      arg[j] = (uint8_t)iHi;
+      OPTa[j + 1] = vHi;
+      E[j + 1] = wHi;
+      prov[j + 1] = keyHi >= 0x10000 ? (uint16_t)((j + 1) << 8) : (uint16_t)keyHi;
+    } else {
+      amb |= 1ull << j;
+      arg[j] = (uint8_t)ibest;
+      OPTa[j + 1] = vbest;
+      const double L = Li1 < Ve ? Li1 : Ve;
+      E[j + 1] = (H - L) * (1.0 + 0x1p-40) + 0x1p-50 * __builtin_fabs(vbest);
+      prov[j + 1] = (uint16_t)((j + 1) << 8);
+    }
+  }
+  if (amb_out) *amb_out = amb;
+  for (int j = n - 1; j >= 0; j = arg[j] - 1)
+    if ((amb >> j) & 1) return false;
+  return true;
+}
+
+// Returns false (and writes nothing final) when LAZY and the pixel needs the exact-OPT DP.
+template <int MAXY, bool LAZY>
+__host__ __device__ bool analyze_pixel(const DevScene& S, const lt_params& P, const lt_tile_in& in,
+                                       const lt_tile_out& out, int64_t p) {
   const int Y = S.n_years;
   const int64_t is = in.stride, os = out.stride;
   int status = LT_ST_OK;
@@ -275,10 +428,14 @@ __host__ __device__ void analyze_pixel(const DevScene& S, const lt_params& P, co
       n++;
     }
     // ---- segmented least squares DP (utils.py:618-631) ----
-    double OPT[MAXY + 1];
     uint8_t arg[MAXY];
-    OPT[0] = 0.0;
-    dp_screened<MAXY>(n, xs, ys, P.line_cost, OPT, arg, status);
+    if constexpr (LAZY) {
+      if (!dp_lazy<MAXY>(n, xs, ys, P.line_cost, arg)) return false;
+    } else {
+      double OPT[MAXY + 1];
+      OPT[0] = 0.0;
+      dp_screened<MAXY>(n, xs, ys, P.line_cost, OPT, arg, status);
+    }
     // ---- find_segments: starts of the optimal segments + the last point ----
     uint64_t vnon = 1ull << (n - 1);  // over non-spike indices
     for (int j = n - 1; j >= 0; j = arg[j] - 1) vnon |= 1ull << arg[j];
@@ -354,6 +511,7 @@ __host__ __device__ void analyze_pixel(const DevScene& S, const lt_params& P, co
 
   rs.write(P, out, p);
   if (out.status) out.status[p] = status;
+  return true;
 }
 
 // Label stage alone (change_labeling on an existing trendline): per slot y, val_fit / vertex /

@@ -121,7 +121,12 @@ class Engine:
         ms = (ctypes.c_double * 2)()
         n = ctypes.c_int64()
         self._check(self.lib.lt_ctx_stage_ms(self.ctx, ms, 2, ctypes.byref(n)), 'stage_ms')
-        return {'winner': ms[0], 'analyze': ms[1], 'launches': n.value}
+        return {'analyze': ms[0], 'resolve': ms[1], 'launches': n.value}
+
+    def last_deferred(self):
+        n = ctypes.c_int64()
+        self._check(self.lib.lt_ctx_last_deferred(self.ctx, ctypes.byref(n)), 'last_deferred')
+        return n.value
 
 
 _ENGINES = {}

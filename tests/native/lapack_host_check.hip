@@ -38,9 +38,22 @@ extern "C" int ltx_analyze_tile(const lt_scene* sc, const lt_params* prm, const 
     S.order[k] = sc->order[k];
     S.dist[k] = sc->dist[k];
   }
+  int deferred = 0;  // same two stages as the GPU: lazy DP, exact-OPT DP for deferred pixels
   for (int64_t p = 0; p < in->n_pix; p++) {
-    if (S.n_years <= 32) lt::analyze_pixel<32>(S, *prm, *in, *out, p);
-    else lt::analyze_pixel<64>(S, *prm, *in, *out, p);
+    bool done = S.n_years <= 32 ? lt::analyze_pixel<32, true>(S, *prm, *in, *out, p)
+                                : lt::analyze_pixel<64, true>(S, *prm, *in, *out, p);
+    if (done) continue;
+    deferred++;
+    if (S.n_years <= 32) lt::analyze_pixel<32, false>(S, *prm, *in, *out, p);
+    else lt::analyze_pixel<64, false>(S, *prm, *in, *out, p);
   }
-  return 0;
+  return deferred;
+}
+
+// Diagnostics: the lazy DP on one compacted series; returns the ambiguous-column mask.
+extern "C" uint64_t ltx_dp_lazy(int n, const uint8_t* xs, const double* ys, double c,
+                                uint8_t* arg, int* deferred) {
+  uint64_t amb = 0;
+  *deferred = !lt::dp_lazy<64>(n, xs, ys, c, arg, &amb);
+  return amb;
 }

@@ -36,8 +36,10 @@ def run_host(hc, scene, params, values, valid):
     tin.obs_valid = valid.ctypes.data_as(_abi.c_u8p) if valid is not None else None
     sc = scene.to_c()
     o = oracle.out_struct(out, P)
-    assert hc.ltx_analyze_tile(ctypes.byref(sc), ctypes.byref(params), ctypes.byref(tin),
-                               ctypes.byref(o)) == 0
+    n_def = hc.ltx_analyze_tile(ctypes.byref(sc), ctypes.byref(params), ctypes.byref(tin),
+                                ctypes.byref(o))
+    assert 0 <= n_def <= P
+    out['_deferred'] = n_def
     return out
 
 
@@ -62,6 +64,7 @@ def test_kernel_code_on_host_matches_oracle_synthetic(hc):
         valid = sc.valid.numpy() if sc.valid is not None else None
         got = run_host(hc, meta, params, vals, valid)
         want = oracle.analyze_tile(meta, params, vals, valid, n_threads=8)
+        print('seed %d: %d of %d pixels deferred to the exact-OPT DP' % (seed, got['_deferred'], 1500))
         for f in want:
             a, b = want[f], got[f]
             same = ((a.view(np.int64) == b.view(np.int64)) | (np.isnan(a) & np.isnan(b))
