@@ -40,7 +40,7 @@ __global__ __launch_bounds__(kBlock) void analyze_kernel(const lt::DevScene* __r
 }
 
 // Stage 1 (wave-lockstep body, lt_fast.h): one wave per workgroup, the pixel series in LDS.
-template <int MAXY>
+template <int MAXY, int RMAX>
 __global__ __launch_bounds__(64) void analyze_fast_kernel(const lt::DevScene* __restrict__ S,
                                                           const lt_params P, const lt_tile_in in,
                                                           const lt_tile_out out,
@@ -50,7 +50,7 @@ __global__ __launch_bounds__(64) void analyze_fast_kernel(const lt::DevScene* __
   const int lane = threadIdx.x;
   const int64_t p = (int64_t)blockIdx.x * 64 + lane;
   const bool live = p < in.n_pix;
-  const bool deferred = !lt::analyze_fast<MAXY>(*S, P, in, out, p, live, lane, L) && live;
+  const bool deferred = !lt::analyze_fast<MAXY, RMAX>(*S, P, in, out, p, live, lane, L) && live;
   const uint64_t mask = __ballot(deferred);
   if (mask == 0) return;
   const int leader = __ffsll((long long)mask) - 1;
@@ -274,15 +274,18 @@ int lt_analyze_tile(lt_ctx* c, const lt_scene* sc, const lt_params* prm, const l
   const int64_t nwave = (in->n_pix + 63) / 64;
   if (nwave > 0x7fffffff) return fail(c, LT_ERR_LIMIT, "tile too large%s");
   dim3 fgrid((unsigned)nwave), fblock(64);
-  if (Y <= 32)
-    hipLaunchKernelGGL(analyze_fast_kernel<32>, fgrid, fblock, 0, stream, c->d_scene, *prm, *in,
-                       *out, c->d_defer, c->d_ndefer);
-  else if (Y <= 48)
-    hipLaunchKernelGGL(analyze_fast_kernel<48>, fgrid, fblock, 0, stream, c->d_scene, *prm, *in,
-                       *out, c->d_defer, c->d_ndefer);
-  else
-    hipLaunchKernelGGL(analyze_fast_kernel<64>, fgrid, fblock, 0, stream, c->d_scene, *prm, *in,
-                       *out, c->d_defer, c->d_ndefer);
+  const bool few = prm->n_rules <= 4;
+#define LT_LAUNCH_FAST(MY, RM)                                                              \
+  hipLaunchKernelGGL((analyze_fast_kernel<MY, RM>), fgrid, fblock, 0, stream, c->d_scene, *prm, \
+                     *in, *out, c->d_defer, c->d_ndefer)
+  if (Y <= 32) {
+    if (few) LT_LAUNCH_FAST(32, 4); else LT_LAUNCH_FAST(32, 16);
+  } else if (Y <= 48) {
+    if (few) LT_LAUNCH_FAST(48, 4); else LT_LAUNCH_FAST(48, 16);
+  } else {
+    if (few) LT_LAUNCH_FAST(64, 4); else LT_LAUNCH_FAST(64, 16);
+  }
+#undef LT_LAUNCH_FAST
   HIP_OR_FAIL(c, hipGetLastError());
   if (ep[0]) HIP_OR_FAIL(c, hipEventRecord(ep[0]->stop, stream));
   if (ep[1]) HIP_OR_FAIL(c, hipEventRecord(ep[1]->start, stream));

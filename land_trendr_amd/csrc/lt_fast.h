@@ -27,7 +27,8 @@ __device__ inline int wave_max(int v) {
 
 template <int MAXY>
 struct WaveLds {
-  double ys[MAXY][64];   // present values (t), compacted in place to non-spike (k); later vertex fits
+  float ys[MAXY][64];    // present values (t), compacted in place to non-spike (k); values that
+                         // are not exact in binary32 send the pixel to the resolve stage
   uint8_t xc[MAXY][64];  // year offset of present point t
   uint8_t sc[MAXY][64];  // scene slot of present point t
   uint8_t xn[MAXY][64];  // year offset of non-spike point k
@@ -37,7 +38,7 @@ struct WaveLds {
 };
 
 // Returns false when the pixel's optimal path crosses an ambiguous DP column (resolve stage).
-template <int MAXY>
+template <int MAXY, int RMAX>
 __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const lt_tile_in& in,
                                    const lt_tile_out& out, int64_t p, bool live, int lane,
                                    WaveLds<MAXY>& L) {
@@ -48,6 +49,7 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
 
   // ---- pick_winners (utils.py:491-521) over wave-uniform year slots ----
   int T = 0, y0 = 0;
+  bool f32_bad = false;
   for (int y = 0; y < Y; y++) {
     int best = -1, bd = 0x7fffffff;
     const int k1 = S.slot_begin[y + 1];
@@ -66,7 +68,9 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
       if (S.feb29_bad[y]) status |= LT_ST_FEB29;
       const double v = in.obs_val[(int64_t)best * is + p];
       if (T == 0) y0 = S.year[y];
-      L.ys[T][lane] = v;
+      const float vf = (float)v;
+      if (!((double)vf == v)) f32_bad = true;
+      L.ys[T][lane] = vf;
       L.xc[T][lane] = (uint8_t)(S.year[y] - y0);
       L.sc[T][lane] = (uint8_t)y;
       T++;
@@ -82,7 +86,9 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
       if (out.vertex) out.vertex[q] = 0;
     }
   }
-  const bool ok = live && T >= 2;
+  // the reference raises for T < 2; non-binary32 values take the resolve stage's double path
+  const bool ok = live && T >= 2 && !f32_bad;
+  double syy_tot = 0.0;
   if (live && T == 0) status |= LT_ST_EMPTY;
   if (live && T == 1) status |= LT_ST_SINGLE_YEAR;
   const int Tmax = wave_max(ok ? T : 0);
@@ -143,7 +149,9 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
     // dropna: compact the non-spike points in place (k <= t)
     for (int t = 0; t < Tmax; t++) {
       if (!(ok && t < T) || ((spike >> t) & 1)) continue;
-      L.ys[n][lane] = L.ys[t][lane];
+      const float yk = L.ys[t][lane];
+      syy_tot = __builtin_fma((double)yk, (double)yk, syy_tot);
+      L.ys[n][lane] = yk;
       L.xn[n][lane] = L.xc[t][lane];
       L.tk[n][lane] = (uint8_t)t;
       n++;
@@ -152,7 +160,7 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
   const int nmax = wave_max(n);
 
   // ---- segmented least squares DP (utils.py:618-631), decided lazily ----
-  bool deferred = false;
+  bool deferred = live && T >= 2 && f32_bad;
   uint64_t vmask = 0;  // vertices over non-spike indices
   if (nmax >= 1) {
     const double c = P.line_cost;
@@ -164,84 +172,80 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
     double Emax = 0.0;       // bound on |OPTa[k] - OPT[k]| for every inexact k so far
     int pv_cur = 0, pv_prev = 0;  // provenance of OPTa[j] and OPTa[j-1]
     uint64_t amb = 0;
+    // Every inexact candidate of a column gets the same half-width: Emax + kScreen * (sum of y^2
+    // over the pixel, >= that of any segment) + the rounding of its own sums (2^-50 |v|).
+    const double wscreen = kScreen * syy_tot;
     for (int j = 0; j < nmax; j++) {
       const bool col = j < n;
       double Sy = 0.0, Sxy = 0.0, Syy = 0.0;
       int Sx = 0, Sxx = 0;
-      double Ve = inf, Hi = inf, Li1 = inf, Li2 = inf, vHi = 0.0, wHi = 0.0, vbest = inf;
-      int ie = 0, iHi = 0, ibest = 0, keyHi = -1, keyL1 = -2;
+      double Ve = inf, v1 = inf, v2 = inf;
+      int ie = 0, i1 = 0, k1 = -1;
 #pragma unroll
       for (int i = MAXY - 1; i >= 0; i--) {
         if (i > j) continue;  // wave-uniform
         const int xi = L.xn[i][lane];
-        const double yi = L.ys[i][lane];
+        const double yi = (double)L.ys[i][lane];
         Sx += xi;
         Sxx += xi * xi;
         Sy += yi;
-        Sxy += (double)xi * yi;
-        Syy += yi * yi;
-        const int m = j - i + 1;
-        const bool ex_i = (exact >> i) & 1;
-        double e = 0.0, w = ex_i ? 0.0 : Emax;
-        if (m >= 3) {
+        Sxy = __builtin_fma((double)xi, yi, Sxy);
+        Syy = __builtin_fma(yi, yi, Syy);
+        const int m = j - i + 1;  // wave-uniform
+        double e = 0.0;
+        if (m >= 3) {  // closed-form SSE: (m*Syy - Sy^2 - N1^2/D) / m, one reciprocal
           const double md = (double)m;
           const double D = (double)(m * Sxx - Sx * Sx);
-          const double t1 = md * Syy - Sy * Sy;
-          const double N1 = md * Sxy - (double)Sx * Sy;
-          e = (t1 - N1 * N1 / D) / md;
+          const double t1 = __builtin_fma(md, Syy, -(Sy * Sy));
+          const double N1 = __builtin_fma(md, Sxy, -((double)Sx * Sy));
+          const double den = md * D;
+          double r = __builtin_amdgcn_rcp(den);
+          r = __builtin_fma(r, __builtin_fma(-den, r, 1.0), r);
+          e = __builtin_fma(t1, D, -(N1 * N1)) * r;
           e = e < 0.0 ? 0.0 : e;
-          w += kScreen * Syy;
         }
         const double v = (e + c) + OPTa[i];
-        if (v <= vbest) {
-          vbest = v;
-          ibest = i;
-        }
-        if (w == 0.0) {
+        if (m < 3 && ((exact >> i) & 1)) {  // reference arithmetic on reference operands
           if (v <= Ve) {
             Ve = v;
             ie = i;
           }
           continue;
         }
-        w += 0x1p-50 * __builtin_fabs(v);
+        // candidates with equal keys have bitwise-equal reference values (and equal v)
         const int key = m >= 3 ? 0x10000 | i : (m == 1 ? pv_cur : pv_prev) + 1;
-        const double lo = v - w, hi = v + w;
-        if (hi <= Hi) {
-          Hi = hi;
-          iHi = i;
-          keyHi = key;
-          vHi = v;
-          wHi = w;
-        }
-        if (lo <= Li1) {
-          if (key != keyL1) Li2 = Li1;
-          Li1 = lo;
-          keyL1 = key;
-        } else if (lo < Li2 && key != keyL1) {
-          Li2 = lo;
+        if (v <= v1) {  // i descends: "<=" keeps the smaller start among equal values
+          if (key != k1) v2 = v1;
+          v1 = v;
+          i1 = i;
+          k1 = key;
+        } else if (v < v2 && key != k1) {
+          v2 = v;
         }
       }
-      const double H = Hi < Ve ? Hi : Ve;
+      const bool any1 = k1 != -1, any2 = v2 != inf;
+      const double w1 = any1 ? Emax + wscreen + 0x1p-50 * __builtin_fabs(v1) : 0.0;
+      const double w2 = any2 ? Emax + wscreen + 0x1p-50 * __builtin_fabs(v2) : 0.0;
+      const double H = any1 && v1 + w1 < Ve ? v1 + w1 : Ve;  // the exact minimum lies below H
       int a;
       double vnew, enew = 0.0;
       int pnew = 0;
       bool exnew = false;
-      if (Li1 > H) {
+      if (!any1 || v1 - w1 > H) {  // no inexact interval reaches H: the exact candidates decide
         a = ie;
         vnew = Ve;
         exnew = true;
-      } else if (keyL1 == keyHi && Li2 > H && Ve > H) {
-        a = iHi;
-        vnew = vHi;
-        enew = wHi;
-        pnew = keyHi >= 0x10000 ? (j + 1) << 8 : keyHi;
+      } else if ((!any2 || v2 - w2 > H) && Ve > H) {  // one value group lies below all others
+        a = i1;
+        vnew = v1;
+        enew = w1;
+        pnew = k1 >= 0x10000 ? (j + 1) << 8 : k1;
       } else {
         if (col) amb |= 1ull << j;
-        a = ibest;
-        vnew = vbest;
-        const double Lo = Li1 < Ve ? Li1 : Ve;
-        enew = (H - Lo) * (1.0 + 0x1p-40) + 0x1p-50 * __builtin_fabs(vbest);
+        a = v1 <= Ve ? i1 : ie;
+        vnew = v1 <= Ve ? v1 : Ve;
+        const double Lo = v1 - w1 < Ve ? v1 - w1 : Ve;
+        enew = (H - Lo) * (1.0 + 0x1p-40) + 0x1p-50 * __builtin_fabs(vnew);
         pnew = (j + 1) << 8;
       }
       if (col) {
@@ -266,13 +270,17 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
       }
     }
   }
-  if (deferred) return false;
+  // deferred lanes stay in the wave (the loops below use wave collectives) but do nothing more
+  if (deferred) vmask = 0;
 
   // ---- vertices2eqns + eqns2fitted_points in lockstep over the vertex number q ----
   int nv = 0;
   for (uint64_t m = vmask; m; m &= m - 1) L.vt[nv++][lane] = (uint8_t)__builtin_ctzll(m);
   const int nvmax = wave_max(nv);
   double pm = 0.0, pb = 0.0;   // eqn of vertex q-1
+  RuleState1 rs[RMAX];
+  double prev_fit = 0.0;
+  int32_t prev_year = 0;
   for (int q = 0; q < nvmax; q++) {
     const bool act = q < nv;
     const int ka = act ? L.vt[q][lane] : 0;
@@ -287,7 +295,8 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
     if (__ballot(has_next)) {
       const int rc = lstsq_segment(
           mseg, [&](int k) { return has_next ? (double)L.xn[kbase + k][lane] : (double)k; },
-          [&](int k) { return has_next ? L.ys[kbase + k][lane] : 0.0; }, true, sm, sbv, ssr);
+          [&](int k) { return has_next ? (double)L.ys[kbase + k][lane] : 0.0; }, true, sm, sbv,
+          ssr);
       if (has_next) {
         if (rc < 0) status |= LT_ST_NUMERIC;
         cm = sm;
@@ -299,7 +308,7 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
     const int tb = has_next ? L.tk[kb][lane] : ta + 1;
     const int span = act ? tb - ta : 0;
     const int spanmax = wave_max(span);
-    const double raw_v = act ? L.ys[ka][lane] : 0.0;
+    const double raw_v = act ? (double)L.ys[ka][lane] : 0.0;
     double fit_vertex = 0.0;
     for (int s = 0; s < spanmax; s++) {
       if (s >= span) continue;
@@ -329,24 +338,30 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
       if (out.spike) out.spike[o] = (uint8_t)((spike >> t) & 1);
       if (out.vertex) out.vertex[o] = s == 0 ? 1 : 0;
     }
-    if (act) L.ys[q][lane] = fit_vertex;  // q <= ka: the raw values still needed sit above q
+    // parse_disturbances / match_rule (classes.py:156-232): the segment ending at vertex q
+    if (act) {
+      const int32_t yr = y0 + L.xn[ka][lane];
+      if (q > 0) {
+#pragma unroll
+        for (int r = 0; r < RMAX; r++)
+          if (r < P.n_rules)
+            rs[r].offer(P.rules[r], P.pre_threshold_mode, prev_year, yr - prev_year, prev_fit,
+                        prev_fit - fit_vertex, status);
+      }
+      prev_fit = fit_vertex;
+      prev_year = yr;
+    }
     pm = cm;
     pb = cb;
   }
 
-  // ---- change_labeling (utils.py:795-820): rules outer, disturbances inner ----
-  for (int r = 0; r < P.n_rules; r++) {
-    RuleState1 rs;
-    for (int q = 1; q < nvmax; q++) {
-      if (q >= nv) continue;
-      const int32_t on = y0 + L.xn[L.vt[q - 1][lane]][lane];
-      const int32_t yr = y0 + L.xn[L.vt[q][lane]][lane];
-      const double f0 = L.ys[q - 1][lane], f1 = L.ys[q][lane];
-      rs.offer(P.rules[r], P.pre_threshold_mode, on, yr - on, f0, f0 - f1, status);
-    }
-    if (live) rs.write(P.rules[r], out, (int64_t)r * os + p);
+  // ---- change_labeling (utils.py:795-820) outputs ----
+  if (live && !deferred) {
+#pragma unroll
+    for (int r = 0; r < RMAX; r++)
+      if (r < P.n_rules) rs[r].write(P.rules[r], out, (int64_t)r * os + p);
   }
-  if (!live) return true;
+  if (!live || deferred) return !deferred;
   if (!ok) {  // the reference raises for this pixel: per-year fields of present years are NaN
     for (int t = 0; t < T; t++) {
       const int64_t o = (int64_t)L.sc[t][lane] * os + p;
