@@ -172,15 +172,12 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
     double Emax = 0.0;       // bound on |OPTa[k] - OPT[k]| for every inexact k so far
     int pv_cur = 0, pv_prev = 0;  // provenance of OPTa[j] and OPTa[j-1]
     uint64_t amb = 0;
-    // Every inexact candidate of a column gets the same half-width: Emax + kScreen * (sum of y^2
-    // over the pixel, >= that of any segment) + the rounding of its own sums (2^-50 |v|).
-    const double wscreen = kScreen * syy_tot;
     for (int j = 0; j < nmax; j++) {
       const bool col = j < n;
       double Sy = 0.0, Sxy = 0.0, Syy = 0.0;
       int Sx = 0, Sxx = 0;
-      double Ve = inf, v1 = inf, v2 = inf;
-      int ie = 0, i1 = 0, k1 = -1;
+      double Ve = inf, Hi = inf, L1 = inf, L2 = inf, v1 = inf, w1 = 0.0;
+      int ie = 0, i1 = 0, k1 = -1, kL = -2;
 #pragma unroll
       for (int i = MAXY - 1; i >= 0; i--) {
         if (i > j) continue;  // wave-uniform
@@ -212,30 +209,38 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
           }
           continue;
         }
-        // candidates with equal keys have bitwise-equal reference values (and equal v)
+        // interval around the reference value: OPT bound + screening bound of this segment +
+        // the rounding of this candidate's own two additions
+        const double w = __builtin_fma(0x1p-50, __builtin_fabs(v),
+                                       __builtin_fma(kScreen, Syy, ((exact >> i) & 1) ? 0.0 : Emax));
+        const double hi = v + w, lo = v - w;
+        // candidates with equal keys have bitwise-equal reference values (and equal v, w)
         const int key = m >= 3 ? 0x10000 | i : (m == 1 ? pv_cur : pv_prev) + 1;
-        if (v <= v1) {  // i descends: "<=" keeps the smaller start among equal values
-          if (key != k1) v2 = v1;
-          v1 = v;
+        if (hi <= Hi) {  // i descends: "<=" keeps the smaller start among equal values
+          Hi = hi;
           i1 = i;
           k1 = key;
-        } else if (v < v2 && key != k1) {
-          v2 = v;
+          v1 = v;
+          w1 = w;
+        }
+        if (lo <= L1) {
+          if (key != kL) L2 = L1;
+          L1 = lo;
+          kL = key;
+        } else if (lo < L2 && key != kL) {
+          L2 = lo;
         }
       }
-      const bool any1 = k1 != -1, any2 = v2 != inf;
-      const double w1 = any1 ? Emax + wscreen + 0x1p-50 * __builtin_fabs(v1) : 0.0;
-      const double w2 = any2 ? Emax + wscreen + 0x1p-50 * __builtin_fabs(v2) : 0.0;
-      const double H = any1 && v1 + w1 < Ve ? v1 + w1 : Ve;  // the exact minimum lies below H
+      const double H = Hi < Ve ? Hi : Ve;  // the exact minimum lies in [min(L1, Ve), H]
       int a;
       double vnew, enew = 0.0;
       int pnew = 0;
       bool exnew = false;
-      if (!any1 || v1 - w1 > H) {  // no inexact interval reaches H: the exact candidates decide
+      if (L1 > H) {  // no inexact interval reaches H: the exact candidates decide
         a = ie;
         vnew = Ve;
         exnew = true;
-      } else if ((!any2 || v2 - w2 > H) && Ve > H) {  // one value group lies below all others
+      } else if (kL == k1 && L2 > H && Ve > H) {  // one value group lies below all others
         a = i1;
         vnew = v1;
         enew = w1;
@@ -244,7 +249,7 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
         if (col) amb |= 1ull << j;
         a = v1 <= Ve ? i1 : ie;
         vnew = v1 <= Ve ? v1 : Ve;
-        const double Lo = v1 - w1 < Ve ? v1 - w1 : Ve;
+        const double Lo = L1 < Ve ? L1 : Ve;
         enew = (H - Lo) * (1.0 + 0x1p-40) + 0x1p-50 * __builtin_fabs(vnew);
         pnew = (j + 1) << 8;
       }
