@@ -7,9 +7,9 @@ synthetic, generated directly in HBM before the timed region.
 
 A step = one pass of the hot path over the rank's whole scene, as a queue of pixel tiles
 (lt_analyze_tile launches on the current stream). Multi-GPU (torchrun, one process per GPU):
-each rank analyses its own scene (weak scaling, no data-path collective); with --gather the
-label rasters are then gathered to rank 0 over RCCL inside the step (the reference's
-output_reducer input).
+each rank analyses its own scene (weak scaling, no data-path collective), then the label
+rasters are gathered to rank 0 over RCCL inside the step (the reference's output_reducer input,
+SURVEY.md §8(e); --no-gather drops it).
 """
 import argparse
 import json
@@ -22,6 +22,7 @@ import torch
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+from land_trendr_amd.distributed import LABEL_GATHER_FIELDS  # noqa: E402
 from land_trendr_amd.engine import get_engine  # noqa: E402
 from land_trendr_amd.scene import build_scene, parse_date  # noqa: E402
 from land_trendr_amd.settings import compile_params  # noqa: E402
@@ -58,7 +59,7 @@ def bytes_per_pixel(cfg, n_obs, n_years):
     inp = n_obs * 8 + (n_obs if cfg['mask'] > 0 else 0)          # f64 index values + mask
     lab = len(cfg['rules']) * (1 + 4 + 4 + 4 + 8)                 # matched/class/onset/dur/mag
     tl = n_years * (6 * 8 + 2 + 2) if cfg['trendline'] else 0     # 6 f64 + spike/vertex + winner
-    return inp + lab + 4                                          # + status
+    return inp + lab + tl + 4                                     # + status
 
 
 def cpu_baseline(cfg, seconds):
@@ -98,7 +99,8 @@ def main():
     ap.add_argument('--config', default='c2', choices=sorted(CONFIGS))
     ap.add_argument('--pixels', type=int, default=0, help='pixels per GPU (default: config)')
     ap.add_argument('--tile', type=int, default=1 << 22, help='pixels per launch')
-    ap.add_argument('--gather', action='store_true', help='RCCL-gather label rasters to rank 0')
+    ap.add_argument('--no-gather', action='store_true',
+                    help='N>1: skip the RCCL gather of label rasters to rank 0')
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     args = ap.parse_args()
@@ -126,9 +128,10 @@ def main():
                    'spike', 'vertex']
     out = eng.alloc_outputs(meta.n_years, params.n_rules, P, fields)
     tiles = [(p0, min(P, p0 + args.tile)) for p0 in range(0, P, args.tile)]
-    gathered = None
-    if dist is not None and args.gather and rank == 0:
-        gathered = [torch.empty_like(out['class_val']) for _ in range(world)]
+    gather = dist is not None and not args.no_gather
+    recv = None
+    if gather and rank == 0:  # the writer's label rasters for the whole job, allocated once
+        recv = {f: [torch.empty_like(out[f]) for _ in range(world)] for f in LABEL_GATHER_FIELDS}
 
     def step():
         for p0, p1 in tiles:
@@ -136,10 +139,9 @@ def main():
             eng.analyze_tile(meta, params, sc.values[:, p0:p1],
                              sc.valid[:, p0:p1] if sc.valid is not None else None,
                              fields, out=view)
-        if dist is not None and args.gather:
-            for f in ('class_val', 'onset_year', 'duration', 'magnitude'):
-                dist.gather(out[f], [torch.empty_like(out[f]) for _ in range(world)]
-                            if rank == 0 else None, dst=0)
+        if gather:  # one RCCL gather per label raster to the writer rank
+            for f in LABEL_GATHER_FIELDS:
+                dist.gather(out[f], recv[f] if rank == 0 else None, dst=0)
 
     for _ in range(args.warmup):
         step()
@@ -184,7 +186,7 @@ def main():
         'data': 'synthetic (SURVEY.md 8(d) generator, seeded, generated in HBM)',
         'config': {'workload': cfg['desc'], 'pixels_per_gpu': P, 'years': cfg['years'],
                    'obs': meta.n_obs, 'rules': len(rules), 'line_cost': cfg['line_cost'],
-                   'tile_pixels': args.tile, 'gather': bool(args.gather and world > 1),
+                   'tile_pixels': args.tile, 'gather': bool(gather),
                    'parallelism': 'pixel tiles, 1 scene per GPU'},
         'roofline': {'bound': 'fp64-valu', 'achieved': round(achieved, 3),
                      'peak': FP64_PEAK_TFLOPS, 'unit': 'TFLOP/s',
