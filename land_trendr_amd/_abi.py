@@ -89,7 +89,8 @@ def load_lib(path=None):
     global _LIB
     if _LIB is not None and path is None:
         return _LIB
-    p = path or LIB_PATH
+    # LT_HIP_LIB: load another build of the same ABI (kernel ablation / A-B timing builds)
+    p = path or os.environ.get('LT_HIP_LIB') or LIB_PATH
     if not os.path.exists(p):
         raise RuntimeError('HIP library %s not built: run __graft_entry__.build() '
                            '(no CPU fallback exists)' % p)

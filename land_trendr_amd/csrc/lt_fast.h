@@ -298,10 +298,10 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
     const int kbase = has_next ? ka : 0;
     double sm = 0.0, sbv = 0.0, ssr = 0.0;
     if (__ballot(has_next)) {
-      const int rc = lstsq_segment(
-          mseg, [&](int k) { return has_next ? (double)L.xn[kbase + k][lane] : (double)k; },
-          [&](int k) { return has_next ? (double)L.ys[kbase + k][lane] : 0.0; }, true, sm, sbv,
-          ssr);
+      const int rc = lstsq_xint(
+          mseg, [&](int k) { return has_next ? (int)L.xn[kbase + k][lane] : k; },
+          [&](int k) { return has_next ? (double)L.ys[kbase + k][lane] : 0.0; }, true, false,
+          sm, sbv, ssr);
       if (has_next) {
         if (rc < 0) status |= LT_ST_NUMERIC;
         cm = sm;

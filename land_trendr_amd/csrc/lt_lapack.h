@@ -485,4 +485,155 @@ __host__ __device__ inline int lstsq_segment(int m, GX X, GY Y, bool want_soluti
   return rank == 2 ? 0 : -3;
 }
 
+// ------------------------------------------------------------------------------------------------
+// The same least_squares for integer x (year offsets 0..255, the only x the analysis produces),
+// with the passes fused: bit-identical to lstsq_segment (tests/test_lapack_emulation.py).
+//   * dnrm2(x[1:]) is an exact integer sum of squares (the x87 accumulators never round below
+//     2^64), so only its sqrt needs the soft-float80 path;
+//   * both dgemv_t of H1 (ones . v1 and y . v1) share one pass, with DGELSD's B == 0 test and
+//     DLARF's nonzero scan folded in;
+//   * the residual pass runs only when need_ssr.
+// x strictly increasing (so v1[k] != 0 for k >= 1) is required and checked (rc -4 otherwise).
+// ------------------------------------------------------------------------------------------------
+__host__ __device__ inline f80 f80_from_u64(uint64_t s) {
+  if (s == 0) return f80{0, 0};
+  const int lz = __builtin_clzll(s);
+  return f80{s << lz, 63 - lz};  // value = sig * 2^(exp - 63) = s
+}
+
+template <class GX, class GY>
+__host__ __device__ inline int lstsq_xint(int m, GX X, GY Y, bool need_solution, bool need_ssr,
+                                          double& slope, double& icpt, double& ssr) {
+  slope = 0.0;
+  icpt = 0.0;
+  ssr = 0.0;
+  const double rcond = 0x1p-52 * (double)(m > 2 ? m : 2);
+  // H1: alpha = x0, ||x[1:]|| from the exact integer sum of squares
+  const int x0 = X(0);
+  uint64_t S = 0;
+  int xprev = x0;
+  for (int k = 1; k < m; k++) {
+    const int xk = X(k);
+    if (xk <= xprev) return -4;
+    xprev = xk;
+    S += (uint64_t)((int64_t)xk * xk);
+  }
+  const double alpha = (double)x0;
+  const double xn = m == 2 ? (double)X(1) : f80_sqrt_to_double(f80_from_u64(S));
+  const double beta1 = -__builtin_copysign(dlapy2(alpha, xn), alpha);  // xn > 0
+  const double tau1 = (beta1 - alpha) / beta1;
+  const double s1 = 1.0 / (alpha - beta1);
+  // pass A: gemv_t(ones, v1) and gemv_t(y, v1) (4 interleaved lanes + FMA tail), B == 0 test
+  const int m3 = m & 3, m1 = m - m3;
+  double A0 = 0.0, A1 = 0.0, A2 = 0.0, A3 = 0.0, Q0 = 0.0, Q1 = 0.0, Q2 = 0.0, Q3 = 0.0;
+  bool anyy = false;
+  double bmax = 0.0;
+  for (int i = 0; i < m1; i += 4) {
+    const double v0 = i == 0 ? 1.0 : (double)X(i) * s1, va = (double)X(i + 1) * s1,
+                 vb = (double)X(i + 2) * s1, vc = (double)X(i + 3) * s1;
+    const double y0 = Y(i), ya = Y(i + 1), yb = Y(i + 2), yc = Y(i + 3);
+    A0 = A0 + v0;
+    A1 = A1 + va;
+    A2 = A2 + vb;
+    A3 = A3 + vc;
+    Q0 = Q0 + y0 * v0;
+    Q1 = Q1 + ya * va;
+    Q2 = Q2 + yb * vb;
+    Q3 = Q3 + yc * vc;
+    bmax = __builtin_fmax(bmax, __builtin_fmax(__builtin_fmax(__builtin_fabs(y0),
+                                                              __builtin_fabs(ya)),
+                                               __builtin_fmax(__builtin_fabs(yb),
+                                                              __builtin_fabs(yc))));
+  }
+  double wo = 0.0, wy = 0.0;
+  if (m1 > 0) {
+    wo = __builtin_fma((A0 + A2) + (A1 + A3), 1.0, 0.0);
+    wy = __builtin_fma((Q0 + Q2) + (Q1 + Q3), 1.0, 0.0);
+  }
+  auto v1 = [&](int k) { return k == 0 ? 1.0 : (double)X(k) * s1; };
+  if (m3 > 0) {
+    const double ta = v1(m1), ya = Y(m1);
+    bmax = __builtin_fmax(bmax, __builtin_fabs(ya));
+    if (m3 == 1) {
+      wo = __builtin_fma(1.0, ta, wo);
+      wy = __builtin_fma(ya, ta, wy);
+    } else {
+      const double tb = v1(m1 + 1), yb = Y(m1 + 1);
+      bmax = __builtin_fmax(bmax, __builtin_fabs(yb));
+      if (m3 == 2) {
+        wo = wo + __builtin_fma(1.0, ta, 1.0 * tb);
+        wy = wy + __builtin_fma(ya, ta, yb * tb);
+      } else {
+        const double tc = v1(m1 + 2), yc = Y(m1 + 2);
+        bmax = __builtin_fmax(bmax, __builtin_fabs(yc));
+        wo = wo + __builtin_fma(1.0, tc, __builtin_fma(1.0, ta, 1.0 * tb));
+        wy = wy + __builtin_fma(yc, tc, __builtin_fma(ya, ta, yb * tb));
+      }
+    }
+  }
+  anyy = bmax != 0.0;
+  if (!anyy) return 0;  // DGELSD: B == 0 -> zero solution, numpy reports no residual
+  if (!(bmax >= 0x1p-970 && bmax <= 0x1p970)) return -1;
+  const double sc = (-tau1) * wo;
+  const double sb = (-tau1) * wy;  // DLARF applies the reflector: some y[k] != 0
+  auto C = [&](int k) { return __builtin_fma(sc, v1(k), 1.0); };
+  auto B = [&](int k) { return __builtin_fma(sb, v1(k), Y(k)); };
+  if (m == 2) {
+    if (!need_solution) return 0;
+    double s0, sI;
+    const int rank = dlalsd2(beta1, C(1), C(0), B(0), B(1), rcond, s0, sI);
+    if (rank < 0) return -1;
+    slope = s0;
+    icpt = sI;
+    return rank == 2 ? 0 : -3;
+  }
+  // pass B: H2 on c[1:], ||c[2:]|| in soft-float80
+  const double r12 = C(0), alpha2 = C(1);
+  const double xn2 = nrm2(m - 2, [&](int k) { return C(k + 2); });
+  double tau2 = 0.0, beta2 = alpha2, s2 = 0.0;
+  if (xn2 != 0.0) {
+    beta2 = -__builtin_copysign(dlapy2(alpha2, xn2), alpha2);
+    tau2 = (beta2 - alpha2) / beta2;
+    s2 = 1.0 / (alpha2 - beta2);
+  }
+  auto v2 = [&](int k) { return k == 0 ? 1.0 : C(k + 1) * s2; };
+  // pass C: DLARF(v2, tau2) on b[1:]
+  int lastv2 = m - 1;
+  double sb2 = 0.0;
+  bool b2_upd = false;
+  if (tau2 != 0.0) {
+    while (lastv2 > 1 && v2(lastv2 - 1) == 0.0) lastv2--;
+    bool any = false;
+    const double w2 = gemv_t1(lastv2, [&](int k) {
+      const double bk = B(k + 1);
+      any = any || bk != 0.0;
+      return bk;
+    }, v2);
+    if (any) {
+      sb2 = (-tau2) * w2;
+      b2_upd = true;
+    }
+  }
+  auto B2 = [&](int k) {
+    const double bk = B(k);
+    return (b2_upd && k - 1 < lastv2) ? __builtin_fma(sb2, v2(k - 1), bk) : bk;
+  };
+  double res = 0.0;
+  if (need_ssr)
+    for (int k = 2; k < m; k++) {
+      const double bk = B2(k);
+      res = res + bk * bk;
+    }
+  int rank = 2;
+  if (need_solution) {
+    double s0, sI;
+    rank = dlalsd2(beta1, beta2, r12, B(0), B2(1), rcond, s0, sI);
+    if (rank < 0) return -1;
+    slope = s0;
+    icpt = sI;
+  }
+  ssr = rank == 2 ? res : 0.0;
+  return rank == 2 ? 0 : -3;
+}
+
 }  // namespace lt

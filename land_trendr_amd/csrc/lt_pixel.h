@@ -212,9 +212,9 @@ __host__ __device__ inline void dp_screened(int n, const uint8_t* xs, const doub
       double e = 0.0;
       if (m >= 3) {
         double sm, sb, ssr;
-        int rc = lstsq_segment(
-            m, [&](int k) { return (double)xs[i + k]; }, [&](int k) { return ys[i + k]; },
-            false, sm, sb, ssr);
+        int rc = lstsq_xint(
+            m, [&](int k) { return (int)xs[i + k]; }, [&](int k) { return ys[i + k]; }, false,
+            true, sm, sb, ssr);
         if (rc < 0) status |= LT_ST_NUMERIC;
         e = ssr;
       }
@@ -456,9 +456,9 @@ __host__ __device__ bool analyze_pixel(const DevScene& S, const lt_params& P, co
           if (later) {  // not the last vertex: LS over [k, next vertex] (label-inclusive)
             const int k2 = __builtin_ctzll(later);
             double sm, sb, ssr;
-            int rc = lstsq_segment(
-                k2 - k + 1, [&](int q) { return (double)xs[k + q]; },
-                [&](int q) { return ys[k + q]; }, true, sm, sb, ssr);
+            int rc = lstsq_xint(
+                k2 - k + 1, [&](int q) { return (int)xs[k + q]; },
+                [&](int q) { return ys[k + q]; }, true, false, sm, sb, ssr);
             if (rc < 0) status |= LT_ST_NUMERIC;
             cm = sm;
             cb = sb;

@@ -57,3 +57,15 @@ extern "C" uint64_t ltx_dp_lazy(int n, const uint8_t* xs, const double* ys, doub
   *deferred = !lt::dp_lazy<64>(n, xs, ys, c, arg, &amb);
   return amb;
 }
+
+// The integer-x fused variant (lstsq_xint) on integer x given as doubles.
+extern "C" int ltx_lstsq_xint(int m, const double* x, const double* y, int need_solution,
+                              int need_ssr, double* out3) {
+  double s, c, r;
+  int rc = lt::lstsq_xint(m, [&](int k) { return (int)x[k]; }, [&](int k) { return y[k]; },
+                          need_solution != 0, need_ssr != 0, s, c, r);
+  out3[0] = s;
+  out3[1] = c;
+  out3[2] = r;
+  return rc;
+}

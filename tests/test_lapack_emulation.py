@@ -96,3 +96,35 @@ def test_soft_float80_nrm2_matches_x87(hc):
         want = abs(x[0]) if n == 1 else float(np.sqrt(tt))
         bad += not golden_io._bits_equal(got, want)
     assert bad == 0
+
+
+def test_integer_x_fused_variant_matches_oracle(hc):
+    """lstsq_xint (fused passes, integer dnrm2 of x) is bit-identical to the oracle."""
+    hc.ltx_lstsq_xint.argtypes = [ctypes.c_int, D, D, ctypes.c_int, ctypes.c_int, D]
+    rng = np.random.default_rng(77)
+    z = dict(np.load(os.path.join(golden_io.GOLDEN, 'lstsq.npz')))
+    cases = [(z['x'][t, :int(z['m'][t])], z['y'][t, :int(z['m'][t])]) for t in range(len(z['m']))]
+    for t in range(20000):
+        m = int(rng.integers(2, 65))
+        x = np.sort(rng.choice(np.arange(0, 256), m, replace=False)).astype(np.float64)
+        kind = t % 3
+        y = (rng.integers(-3000, 3000, m).astype(np.float64) if kind == 0 else
+             rng.normal(0, 1, m) * 10.0 ** rng.integers(-8, 9) if kind == 1 else
+             rng.integers(0, 3, m).astype(np.float64))
+        cases.append((x, y))
+    bad = 0
+    for x, y in cases:
+        x = np.ascontiguousarray(x, np.float64)
+        y = np.ascontiguousarray(y, np.float64)
+        want = oracle.lstsq(x, y)
+        for sol, ssr in ((1, 1), (1, 0), (0, 1)):
+            o = (ctypes.c_double * 3)()
+            rc = hc.ltx_lstsq_xint(len(x), x.ctypes.data_as(D), y.ctypes.data_as(D), sol, ssr,
+                                   ctypes.cast(o, D))
+            assert rc == want[0]
+            if sol:
+                bad += not (golden_io._bits_equal(o[0], want[1]) and
+                            golden_io._bits_equal(o[1], want[2]))
+            if ssr:
+                bad += not golden_io._bits_equal(o[2], want[3])
+    assert bad == 0
