@@ -15,14 +15,16 @@
 
 namespace lt {
 
-// max over the 64 lanes of a wave (every lane must call it)
+// max over the 64 lanes of a wave (every lane must call it). readfirstlane makes the result an
+// SGPR value, so loops bounded by it are wave-uniform to the compiler: scalar branches instead
+// of exec-mask juggling for every test on the loop counter.
 __device__ inline int wave_max(int v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     const int u = __shfl_xor(v, o);
     v = u > v ? u : v;
   }
-  return v;
+  return __builtin_amdgcn_readfirstlane(v);
 }
 
 template <int MAXY>
@@ -172,7 +174,8 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
     double Emax = 0.0;       // bound on |OPTa[k] - OPT[k]| for every inexact k so far
     int pv_cur = 0, pv_prev = 0;  // provenance of OPTa[j] and OPTa[j-1]
     uint64_t amb = 0;
-    for (int j = 0; j < nmax; j++) {
+    for (int jj = 0; jj < nmax; jj++) {
+      const int j = __builtin_amdgcn_readfirstlane(jj);  // column index in an SGPR
       const bool col = j < n;
       double Sy = 0.0, Sxy = 0.0, Syy = 0.0;
       int Sx = 0, Sxx = 0;
@@ -209,10 +212,13 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
           }
           continue;
         }
-        // interval around the reference value: OPT bound + screening bound of this segment +
-        // the rounding of this candidate's own two additions
+        // interval around the reference value: OPT bound + screening bound of this segment (1-2
+        // point residuals are exactly 0: no screening term, so candidates with equal keys get
+        // equal intervals and the first-minimum rule keeps the smaller start) + the rounding
+        // of this candidate's own two additions
+        const double wopt = ((exact >> i) & 1) ? 0.0 : Emax;
         const double w = __builtin_fma(0x1p-50, __builtin_fabs(v),
-                                       __builtin_fma(kScreen, Syy, ((exact >> i) & 1) ? 0.0 : Emax));
+                                       m >= 3 ? __builtin_fma(kScreen, Syy, wopt) : wopt);
         const double hi = v + w, lo = v - w;
         // candidates with equal keys have bitwise-equal reference values (and equal v, w)
         const int key = m >= 3 ? 0x10000 | i : (m == 1 ? pv_cur : pv_prev) + 1;
