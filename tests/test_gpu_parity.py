@@ -104,6 +104,49 @@ def test_tie_heavy_small_integers_tiny_line_cost_vs_oracle(engine):
             assert same.all(), (lc, f, int((~same).sum()))
 
 
+@pytest.mark.parametrize('cfg', ['c2', 'c3', 'c5'])
+def test_full_size_scene_sampled_vs_oracle(engine, cfg):
+    """BASELINE.json sizes: a 7000x7000-pixel scene per config analysed on the GPU in 4 Mpx
+    tiles (as bench.py does); 20,000 random pixels re-analysed by the oracle must agree bit for
+    bit, every pixel's status must be 0 (no unemulated path), and the label rasters must be
+    internally consistent (matched <=> class_val/onset/duration/magnitude set)."""
+    import bench
+    from land_trendr_amd.synth import make_scene
+    from oracle import oracle
+    c = bench.CONFIGS[cfg]
+    P = c['pixels']
+    sc = make_scene(P, n_years=c['years'], k_min=c['k'][0], k_max=c['k'][1],
+                    mask_prob=c['mask'], seed=2024, device=engine.device)
+    meta = build_scene(sc.dates, parse_date('2014-07-01'))
+    params, _ = compile_params(c['line_cost'], c['rules'], c['mode'])
+    fields = ('status', 'matched', 'class_val', 'onset_year', 'duration', 'magnitude',
+              'val_fit', 'vertex')
+    out = engine.alloc_outputs(meta.n_years, params.n_rules, P, fields)
+    tile = 1 << 22
+    for p0 in range(0, P, tile):
+        p1 = min(P, p0 + tile)
+        engine.analyze_tile(meta, params, sc.values[:, p0:p1],
+                            sc.valid[:, p0:p1] if sc.valid is not None else None, fields,
+                            out={f: t[..., p0:p1] for f, t in out.items()})
+    torch.cuda.synchronize()
+    assert int((out['status'] != 0).sum()) == 0
+    m = out['matched'].bool()
+    assert bool(((out['class_val'] != -99) == m).all())
+    assert bool(((out['duration'] > 0) | ~m).all())
+    idx = torch.from_numpy(np.random.default_rng(7).choice(P, 20000, replace=False)).to(
+        engine.device)
+    vals = sc.values[:, idx].cpu().numpy()
+    valid = sc.valid[:, idx].cpu().numpy() if sc.valid is not None else None
+    want = oracle.analyze_tile(meta, params, vals, valid, n_threads=os.cpu_count() or 1)
+    for f in fields:
+        a, b = want[f], out[f][..., idx].cpu().numpy()
+        same = ((a.view(np.int64) == b.view(np.int64)) | (np.isnan(a) & np.isnan(b))
+                if a.dtype.kind == 'f' else a == b)
+        assert same.all(), (cfg, f, int((~same).sum()))
+    del sc, out
+    torch.cuda.empty_cache()
+
+
 def test_strided_tile_and_subset_outputs(engine):
     """Tiles carved from a larger stack (stride > n_pix) and NULL outputs."""
     g = golden_io.GoldenScene('c1')
