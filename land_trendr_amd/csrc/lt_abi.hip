@@ -46,11 +46,12 @@ __global__ __launch_bounds__(64) void analyze_fast_kernel(const lt::DevScene* __
                                                           const lt_tile_out out,
                                                           int64_t* __restrict__ defer,
                                                           unsigned long long* __restrict__ n_defer) {
-  __shared__ lt::WaveLds<MAXY> L;
+  __shared__ lt::WaveLds<MAXY, float> L;
   const int lane = threadIdx.x;
   const int64_t p = (int64_t)blockIdx.x * 64 + lane;
   const bool live = p < in.n_pix;
-  const bool deferred = !lt::analyze_fast<MAXY, RMAX>(*S, P, in, out, p, live, lane, L) && live;
+  const bool deferred =
+      !lt::analyze_fast<MAXY, RMAX, false, float>(*S, P, in, out, p, live, lane, L) && live;
   const uint64_t mask = __ballot(deferred);
   if (mask == 0) return;
   const int leader = __ffsll((long long)mask) - 1;
@@ -60,7 +61,26 @@ __global__ __launch_bounds__(64) void analyze_fast_kernel(const lt::DevScene* __
   if (deferred) defer[base + __popcll(mask & ((1ull << lane) - 1))] = p;
 }
 
-// Stage 2: the deferred pixels with the exact-OPT screened DP (grid-stride over the list).
+// Stage 2 (wave-lockstep, lt_fast.h with EXACT): the deferred pixels, binary64 series in LDS,
+// exact-OPT DP. A fixed grid strides over the list in whole waves.
+template <int MAXY, int RMAX>
+__global__ __launch_bounds__(64) void resolve_fast_kernel(const lt::DevScene* __restrict__ S,
+                                                          const lt_params P, const lt_tile_in in,
+                                                          const lt_tile_out out,
+                                                          const int64_t* __restrict__ defer,
+                                                          const unsigned long long* __restrict__ n_defer) {
+  __shared__ lt::WaveLds<MAXY, double> L;
+  const int lane = threadIdx.x;
+  const int64_t n = (int64_t)*n_defer;
+  for (int64_t base = (int64_t)blockIdx.x * 64; base < n; base += (int64_t)gridDim.x * 64) {
+    const int64_t k = base + lane;
+    const bool live = k < n;
+    lt::analyze_fast<MAXY, RMAX, true, double>(*S, P, in, out, live ? defer[k] : 0, live, lane,
+                                               L);
+  }
+}
+
+// Stage 2 (per-lane reference body, lt_pixel.h): kept for the host harness's structure.
 template <int MAXY>
 __global__ __launch_bounds__(kBlock) void resolve_kernel(const lt::DevScene* __restrict__ S,
                                                          const lt_params P, const lt_tile_in in,
@@ -265,11 +285,6 @@ int lt_analyze_tile(lt_ctx* c, const lt_scene* sc, const lt_params* prm, const l
     ep[0] = &c->pool[c->used++];
     ep[1] = &c->pool[c->used++];
   }
-  const int64_t nblk = (in->n_pix + kBlock - 1) / kBlock;
-  if (nblk > 0x7fffffff) return fail(c, LT_ERR_LIMIT, "tile too large%s");
-  dim3 grid((unsigned)nblk), block(kBlock);
-  // resolve stage: a fixed grid striding over however many pixels were deferred
-  dim3 rgrid((unsigned)(nblk < 2048 ? nblk : 2048));
   if (ep[0]) HIP_OR_FAIL(c, hipEventRecord(ep[0]->start, stream));
   const int64_t nwave = (in->n_pix + 63) / 64;
   if (nwave > 0x7fffffff) return fail(c, LT_ERR_LIMIT, "tile too large%s");
@@ -289,12 +304,18 @@ int lt_analyze_tile(lt_ctx* c, const lt_scene* sc, const lt_params* prm, const l
   HIP_OR_FAIL(c, hipGetLastError());
   if (ep[0]) HIP_OR_FAIL(c, hipEventRecord(ep[0]->stop, stream));
   if (ep[1]) HIP_OR_FAIL(c, hipEventRecord(ep[1]->start, stream));
-  if (Y <= 32)
-    hipLaunchKernelGGL(resolve_kernel<32>, rgrid, block, 0, stream, c->d_scene, *prm, *in, *out,
-                       c->d_defer, c->d_ndefer);
-  else
-    hipLaunchKernelGGL(resolve_kernel<64>, rgrid, block, 0, stream, c->d_scene, *prm, *in, *out,
-                       c->d_defer, c->d_ndefer);
+  dim3 rg((unsigned)(nwave < 1536 ? nwave : 1536));
+#define LT_LAUNCH_RESOLVE(MY, RM)                                                            \
+  hipLaunchKernelGGL((resolve_fast_kernel<MY, RM>), rg, fblock, 0, stream, c->d_scene, *prm, \
+                     *in, *out, c->d_defer, c->d_ndefer)
+  if (Y <= 32) {
+    if (few) LT_LAUNCH_RESOLVE(32, 4); else LT_LAUNCH_RESOLVE(32, 16);
+  } else if (Y <= 48) {
+    if (few) LT_LAUNCH_RESOLVE(48, 4); else LT_LAUNCH_RESOLVE(48, 16);
+  } else {
+    if (few) LT_LAUNCH_RESOLVE(64, 4); else LT_LAUNCH_RESOLVE(64, 16);
+  }
+#undef LT_LAUNCH_RESOLVE
   HIP_OR_FAIL(c, hipGetLastError());
   if (ep[1]) HIP_OR_FAIL(c, hipEventRecord(ep[1]->stop, stream));
   c->launches++;

@@ -27,10 +27,11 @@ __device__ inline int wave_max(int v) {
   return __builtin_amdgcn_readfirstlane(v);
 }
 
-template <int MAXY>
+// VT: storage type of the series. The analyze stage stores binary32 (pixels whose values are not
+// exact in binary32 are sent to the resolve stage), the resolve stage binary64.
+template <int MAXY, class VT>
 struct WaveLds {
-  float ys[MAXY][64];    // present values (t), compacted in place to non-spike (k); values that
-                         // are not exact in binary32 send the pixel to the resolve stage
+  VT ys[MAXY][64];       // present values (t), compacted in place to non-spike (k)
   uint8_t xc[MAXY][64];  // year offset of present point t
   uint8_t sc[MAXY][64];  // scene slot of present point t
   uint8_t xn[MAXY][64];  // year offset of non-spike point k
@@ -39,11 +40,14 @@ struct WaveLds {
   uint8_t vt[MAXY][64];  // non-spike index of vertex q
 };
 
-// Returns false when the pixel's optimal path crosses an ambiguous DP column (resolve stage).
-template <int MAXY, int RMAX>
+// EXACT = false (analyze stage): the lazy DP; returns false when the pixel's optimal path crosses
+// an ambiguous DP column (or its values are not exact in binary32) — the resolve stage redoes it.
+// EXACT = true (resolve stage): the exact-OPT DP, every column decided with the emulated LAPACK
+// residual of each start inside the error window; always returns true.
+template <int MAXY, int RMAX, bool EXACT, class VT>
 __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const lt_tile_in& in,
                                    const lt_tile_out& out, int64_t p, bool live, int lane,
-                                   WaveLds<MAXY>& L) {
+                                   WaveLds<MAXY, VT>& L) {
   const int Y = S.n_years;
   const int64_t is = in.stride, os = out.stride;
   const double nan = __builtin_nan("");
@@ -70,9 +74,11 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
       if (S.feb29_bad[y]) status |= LT_ST_FEB29;
       const double v = in.obs_val[(int64_t)best * is + p];
       if (T == 0) y0 = S.year[y];
-      const float vf = (float)v;
-      if (!((double)vf == v)) f32_bad = true;
-      L.ys[T][lane] = vf;
+      const VT vs = (VT)v;
+      if constexpr (!EXACT) {
+        if (!((double)vs == v)) f32_bad = true;
+      }
+      L.ys[T][lane] = vs;
       L.xc[T][lane] = (uint8_t)(S.year[y] - y0);
       L.sc[T][lane] = (uint8_t)y;
       T++;
@@ -90,7 +96,6 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
   }
   // the reference raises for T < 2; non-binary32 values take the resolve stage's double path
   const bool ok = live && T >= 2 && !f32_bad;
-  double syy_tot = 0.0;
   if (live && T == 0) status |= LT_ST_EMPTY;
   if (live && T == 1) status |= LT_ST_SINGLE_YEAR;
   const int Tmax = wave_max(ok ? T : 0);
@@ -151,9 +156,7 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
     // dropna: compact the non-spike points in place (k <= t)
     for (int t = 0; t < Tmax; t++) {
       if (!(ok && t < T) || ((spike >> t) & 1)) continue;
-      const float yk = L.ys[t][lane];
-      syy_tot = __builtin_fma((double)yk, (double)yk, syy_tot);
-      L.ys[n][lane] = yk;
+      L.ys[n][lane] = L.ys[t][lane];
       L.xn[n][lane] = L.xc[t][lane];
       L.tk[n][lane] = (uint8_t)t;
       n++;
@@ -164,7 +167,101 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
   // ---- segmented least squares DP (utils.py:618-631), decided lazily ----
   bool deferred = live && T >= 2 && f32_bad;
   uint64_t vmask = 0;  // vertices over non-spike indices
-  if (nmax >= 1) {
+  if constexpr (EXACT) {
+    // ---- exact-OPT DP: closed-form intervals, then the emulated LAPACK residual for every
+    // start whose interval reaches the column's smallest upper bound; first exact minimum ----
+    const double c = P.line_cost;
+    const double inf = __builtin_inf();
+    double OPT[MAXY + 1];
+    double lo[MAXY];
+#pragma unroll
+    for (int k = 0; k <= MAXY; k++) OPT[k] = 0.0;
+    for (int jj = 0; jj < nmax; jj++) {
+      const int j = __builtin_amdgcn_readfirstlane(jj);
+      const bool col = j < n;
+      double Sy = 0.0, Sxy = 0.0, Syy = 0.0;
+      int Sx = 0, Sxx = 0;
+      double H = inf;
+#pragma unroll
+      for (int i = MAXY - 1; i >= 0; i--) {
+        if (i > j) continue;  // wave-uniform
+        const int xi = L.xn[i][lane];
+        const double yi = (double)L.ys[i][lane];
+        Sx += xi;
+        Sxx += xi * xi;
+        Sy += yi;
+        Sxy = __builtin_fma((double)xi, yi, Sxy);
+        Syy = __builtin_fma(yi, yi, Syy);
+        const int m = j - i + 1;
+        double e = 0.0, w = 0.0;  // m <= 2: exact residual 0 on an exact OPT: v is the reference
+        if (m >= 3) {
+          const double md = (double)m;
+          const double D = (double)(m * Sxx - Sx * Sx);
+          const double t1 = __builtin_fma(md, Syy, -(Sy * Sy));
+          const double N1 = __builtin_fma(md, Sxy, -((double)Sx * Sy));
+          const double den = md * D;
+          double r = __builtin_amdgcn_rcp(den);
+          r = __builtin_fma(r, __builtin_fma(-den, r, 1.0), r);
+          e = __builtin_fma(t1, D, -(N1 * N1)) * r;
+          e = e < 0.0 ? 0.0 : e;
+        }
+        const double v = (e + c) + OPT[i];
+        if (m >= 3) w = __builtin_fma(0x1p-50, __builtin_fabs(v), kScreen * Syy);
+        lo[i] = v - w;
+        H = v + w < H ? v + w : H;
+      }
+      uint64_t cand = 0;  // starts whose interval reaches H: the exact minimum is among them
+#pragma unroll
+      for (int i = 0; i < MAXY; i++)
+        if (i <= j && lo[i] <= H) cand |= 1ull << i;
+      const int nc = col ? __builtin_popcountll(cand) : 0;
+      const int ncmax = wave_max(nc);
+      double best = inf;
+      int bi = 0;
+      for (int r = 0; r < ncmax; r++) {  // candidates in increasing start order, lockstep
+        const bool act = r < nc;
+        const int i = act ? __builtin_ctzll(cand) : 0;
+        if (act) cand &= cand - 1;
+        const int m = j - i + 1;
+        const bool ls = act && m >= 3;
+        double e = 0.0;
+        if (__ballot(ls)) {
+          double sm, sb, ssr;
+          const int rc = lstsq_xint(
+              ls ? m : 2, [&](int k) { return ls ? (int)L.xn[i + k][lane] : k; },
+              [&](int k) { return ls ? (double)L.ys[i + k][lane] : 0.0; }, false, true, sm, sb,
+              ssr);
+          if (ls) {
+            if (rc < 0) status |= LT_ST_NUMERIC;
+            e = ssr;
+          }
+        }
+        double o = 0.0;
+#pragma unroll
+        for (int k = 0; k < MAXY; k++)
+          if (k == i) o = OPT[k];  // per-lane index: select chain
+        const double v = (e + c) + o;
+        if (act && v < best) {  // increasing start order + strict "<": the first minimum
+          best = v;
+          bi = i;
+        }
+      }
+      if (col) {
+        L.ag[j][lane] = (uint8_t)bi;
+#pragma unroll
+        for (int k = 1; k <= MAXY; k++)
+          if (k == j + 1) OPT[k] = best;  // wave-uniform index
+      }
+    }
+    if (n >= 1) {
+      vmask = 1ull << (n - 1);
+      for (int j = n - 1; j >= 0;) {
+        const int a = L.ag[j][lane];
+        vmask |= 1ull << a;
+        j = a - 1;
+      }
+    }
+  } else if (nmax >= 1) {
     const double c = P.line_cost;
     const double inf = __builtin_inf();
     double OPTa[MAXY + 1];
