@@ -32,12 +32,10 @@ __device__ inline int wave_max(int v) {
 template <int MAXY, class VT>
 struct WaveLds {
   VT ys[MAXY][64];       // present values (t), compacted in place to non-spike (k)
-  uint8_t xc[MAXY][64];  // year offset of present point t
   uint8_t sc[MAXY][64];  // scene slot of present point t
   uint8_t xn[MAXY][64];  // year offset of non-spike point k
-  uint8_t tk[MAXY][64];  // present index t of non-spike point k
-  uint8_t ag[MAXY][64];  // DP argmin of column k
-  uint8_t vt[MAXY][64];  // non-spike index of vertex q
+  uint8_t ag[MAXY][64];  // DP argmin of column k; after the backtrack: non-spike index of vertex q
+  int32_t year[LT_MAX_YEARS];  // the scene's calendar year per slot (64 words: one bank each)
 };
 
 // EXACT = false (analyze stage): the lazy DP; returns false when the pixel's optimal path crosses
@@ -52,6 +50,9 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
   const int64_t is = in.stride, os = out.stride;
   const double nan = __builtin_nan("");
   int status = LT_ST_OK;
+  static_assert(LT_MAX_YEARS == 64, "one year-table word per lane");
+  if (lane < Y) L.year[lane] = S.year[lane];
+  __syncthreads();  // one wave per workgroup: orders the table writes before any lane reads
 
   // ---- pick_winners (utils.py:491-521) over wave-uniform year slots ----
   int T = 0, y0 = 0;
@@ -79,7 +80,6 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
         if (!((double)vs == v)) f32_bad = true;
       }
       L.ys[T][lane] = vs;
-      L.xc[T][lane] = (uint8_t)(S.year[y] - y0);
       L.sc[T][lane] = (uint8_t)y;
       T++;
       if (out.val_raw) out.val_raw[q] = v;
@@ -157,8 +157,7 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
     for (int t = 0; t < Tmax; t++) {
       if (!(ok && t < T) || ((spike >> t) & 1)) continue;
       L.ys[n][lane] = L.ys[t][lane];
-      L.xn[n][lane] = L.xc[t][lane];
-      L.tk[n][lane] = (uint8_t)t;
+      L.xn[n][lane] = (uint8_t)(L.year[L.sc[t][lane]] - y0);
       n++;
     }
   }
@@ -383,17 +382,18 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
 
   // ---- vertices2eqns + eqns2fitted_points in lockstep over the vertex number q ----
   int nv = 0;
-  for (uint64_t m = vmask; m; m &= m - 1) L.vt[nv++][lane] = (uint8_t)__builtin_ctzll(m);
+  for (uint64_t m = vmask; m; m &= m - 1) L.ag[nv++][lane] = (uint8_t)__builtin_ctzll(m);
   const int nvmax = wave_max(nv);
   double pm = 0.0, pb = 0.0;   // eqn of vertex q-1
   RuleState1 rs[RMAX];
   double prev_fit = 0.0;
   int32_t prev_year = 0;
+  int ta = 0;                  // present index of vertex q (vertex 0 is the first point)
   for (int q = 0; q < nvmax; q++) {
     const bool act = q < nv;
-    const int ka = act ? L.vt[q][lane] : 0;
+    const int ka = act ? L.ag[q][lane] : 0;
     const bool has_next = act && q + 1 < nv;
-    const int kb = has_next ? L.vt[q + 1][lane] : ka;
+    const int kb = has_next ? L.ag[q + 1][lane] : ka;
     double cm = pm, cb = pb;
     // one LAPACK-emulated fit per vertex number for the whole wave (lanes without a next
     // vertex reuse the previous equation, utils.py:662)
@@ -411,17 +411,23 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
         cb = sbv;
       }
     }
-    // emit the vertex point and the points up to the next vertex (spikes included)
-    const int ta = act ? L.tk[ka][lane] : 0;
-    const int tb = has_next ? L.tk[kb][lane] : ta + 1;
-    const int span = act ? tb - ta : 0;
-    const int spanmax = wave_max(span);
+    // emit the vertex point and the points up to the next vertex (spikes included): walk the
+    // present points from the vertex, counting non-spike ones until the next vertex
     const double raw_v = act ? (double)L.ys[ka][lane] : 0.0;
     double fit_vertex = 0.0;
-    for (int s = 0; s < spanmax; s++) {
-      if (s >= span) continue;
-      const int t = ta + s;
-      const double x = (double)L.xc[t][lane];
+    int t = ta, kk = ka;
+    bool going = act;
+    for (int s = 0; __ballot(going); s++) {
+      if (!going) continue;
+      if (s > 0) {
+        const bool nonspike = t >= 64 || !((spike >> t) & 1);
+        if (!has_next || (nonspike && ++kk == kb)) {  // the next vertex, or the last one done
+          going = false;
+          ta = t;
+          continue;
+        }
+      }
+      const double x = (double)(L.year[L.sc[t][lane]] - y0);
       double fv, fmv, fbv;
       if (s == 0 && q > 0 && !(pm == cm && pb == cb)) {
         const double fl = (pm * x) + pb;
@@ -445,6 +451,7 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
       if (out.right_b) out.right_b[o] = cb;
       if (out.spike) out.spike[o] = (uint8_t)((spike >> t) & 1);
       if (out.vertex) out.vertex[o] = s == 0 ? 1 : 0;
+      t++;
     }
     // parse_disturbances / match_rule (classes.py:156-232): the segment ending at vertex q
     if (act) {
