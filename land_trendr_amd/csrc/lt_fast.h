@@ -268,15 +268,17 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
     for (int k = 0; k <= MAXY; k++) OPTa[k] = 0.0;
     uint64_t exact = 1;      // bit k: OPTa[k] is the reference value itself
     double Emax = 0.0;       // bound on |OPTa[k] - OPT[k]| for every inexact k so far
-    int pv_cur = 0, pv_prev = 0;  // provenance of OPTa[j] and OPTa[j-1]
+    double opt_j = 0.0, opt_jm1 = 0.0;  // OPTa[j] and OPTa[j-1] (the 1- and 2-point starts)
     uint64_t amb = 0;
     for (int jj = 0; jj < nmax; jj++) {
       const int j = __builtin_amdgcn_readfirstlane(jj);  // column index in an SGPR
       const bool col = j < n;
       double Sy = 0.0, Sxy = 0.0, Syy = 0.0;
       int Sx = 0, Sxx = 0;
-      double Ve = inf, Hi = inf, L1 = inf, L2 = inf, v1 = inf, w1 = 0.0;
-      int ie = 0, i1 = 0, k1 = -1, kL = -2;
+      // interval candidates: smallest upper end (Hi: start i1, value v1) and the two smallest
+      // lower ends (L1 at start iL, L2); Ve/ie: the exact candidates
+      double Ve = inf, Hi = inf, L1 = inf, L2 = inf, v1 = inf;
+      int ie = 0, i1 = 0, iL = -1;
 #pragma unroll
       for (int i = MAXY - 1; i >= 0; i--) {
         if (i > j) continue;  // wave-uniform
@@ -287,73 +289,79 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
         Sy += yi;
         Sxy = __builtin_fma((double)xi, yi, Sxy);
         Syy = __builtin_fma(yi, yi, Syy);
-        const int m = j - i + 1;  // wave-uniform
-        double e = 0.0;
-        if (m >= 3) {  // closed-form SSE: (m*Syy - Sy^2 - N1^2/D) / m, one reciprocal
-          const double md = (double)m;
-          const double D = (double)(m * Sxx - Sx * Sx);
-          const double t1 = __builtin_fma(md, Syy, -(Sy * Sy));
-          const double N1 = __builtin_fma(md, Sxy, -((double)Sx * Sy));
-          const double den = md * D;
-          double r = __builtin_amdgcn_rcp(den);
-          r = __builtin_fma(r, __builtin_fma(-den, r, 1.0), r);
-          e = __builtin_fma(t1, D, -(N1 * N1)) * r;
-          e = e < 0.0 ? 0.0 : e;
-        }
+        if (i + 2 > j) continue;  // the 1- and 2-point starts are priced after the loop
+        // closed-form SSE: (m*Syy - Sy^2 - N1^2/D) / m, one reciprocal
+        const int m = j - i + 1;  // wave-uniform, >= 3
+        const double md = (double)m;
+        const double D = (double)(m * Sxx - Sx * Sx);
+        const double t1 = __builtin_fma(md, Syy, -(Sy * Sy));
+        const double N1 = __builtin_fma(md, Sxy, -((double)Sx * Sy));
+        const double den = md * D;
+        double r = __builtin_amdgcn_rcp(den);
+        r = __builtin_fma(r, __builtin_fma(-den, r, 1.0), r);
+        const double e = __builtin_fmax(__builtin_fma(t1, D, -(N1 * N1)) * r, 0.0);
         const double v = (e + c) + OPTa[i];
-        if (m < 3 && ((exact >> i) & 1)) {  // reference arithmetic on reference operands
-          if (v <= Ve) {
+        // interval around the reference value: OPT bound + screening bound of this segment +
+        // the rounding of this candidate's own two additions
+        const double wopt = ((exact >> i) & 1) ? 0.0 : Emax;
+        const double w = __builtin_fma(0x1p-50, __builtin_fabs(v), __builtin_fma(kScreen, Syy, wopt));
+        const double hi = v + w, lo = v - w;
+        if (hi <= Hi) {  // i descends: "<=" keeps the smaller start among equal upper ends
+          i1 = i;
+          v1 = v;
+        }
+        Hi = hi <= Hi ? hi : Hi;
+        const bool bl = lo <= L1;
+        L2 = bl ? L1 : (lo < L2 ? lo : L2);
+        L1 = bl ? lo : L1;
+        iL = bl ? i : iL;
+      }
+      // the 2-point then the 1-point start (larger starts than every start above: strict "<"
+      // keeps the first minimum). Their residuals are exactly 0, so with an exact OPTa the
+      // value is the reference's own; otherwise an interval of half-width Emax + rounding.
+#pragma unroll
+      for (int s = 1; s >= 0; s--) {
+        const int i = j - s;
+        if (i < 0) continue;  // wave-uniform
+        const double v = c + (s ? opt_jm1 : opt_j);
+        if ((exact >> i) & 1) {
+          if (v < Ve) {
             Ve = v;
             ie = i;
           }
-          continue;
-        }
-        // interval around the reference value: OPT bound + screening bound of this segment (1-2
-        // point residuals are exactly 0: no screening term, so candidates with equal keys get
-        // equal intervals and the first-minimum rule keeps the smaller start) + the rounding
-        // of this candidate's own two additions
-        const double wopt = ((exact >> i) & 1) ? 0.0 : Emax;
-        const double w = __builtin_fma(0x1p-50, __builtin_fabs(v),
-                                       m >= 3 ? __builtin_fma(kScreen, Syy, wopt) : wopt);
-        const double hi = v + w, lo = v - w;
-        // candidates with equal keys have bitwise-equal reference values (and equal v, w)
-        const int key = m >= 3 ? 0x10000 | i : (m == 1 ? pv_cur : pv_prev) + 1;
-        if (hi <= Hi) {  // i descends: "<=" keeps the smaller start among equal values
-          Hi = hi;
-          i1 = i;
-          k1 = key;
-          v1 = v;
-          w1 = w;
-        }
-        if (lo <= L1) {
-          if (key != kL) L2 = L1;
-          L1 = lo;
-          kL = key;
-        } else if (lo < L2 && key != kL) {
-          L2 = lo;
+        } else {
+          const double w = __builtin_fma(0x1p-50, __builtin_fabs(v), Emax);
+          const double hi = v + w, lo = v - w;
+          if (hi < Hi) {
+            i1 = i;
+            v1 = v;
+          }
+          Hi = hi < Hi ? hi : Hi;
+          const bool bl = lo <= L1;
+          L2 = bl ? L1 : (lo < L2 ? lo : L2);
+          L1 = bl ? lo : L1;
+          iL = bl ? i : iL;
         }
       }
       const double H = Hi < Ve ? Hi : Ve;  // the exact minimum lies in [min(L1, Ve), H]
       int a;
       double vnew, enew = 0.0;
-      int pnew = 0;
       bool exnew = false;
       if (L1 > H) {  // no inexact interval reaches H: the exact candidates decide
         a = ie;
         vnew = Ve;
         exnew = true;
-      } else if (kL == k1 && L2 > H && Ve > H) {  // one value group lies below all others
+      } else if (iL == i1 && L2 > H && Ve > H) {  // one candidate lies below all others
         a = i1;
         vnew = v1;
-        enew = w1;
-        pnew = k1 >= 0x10000 ? (j + 1) << 8 : k1;
+        // its half-width, rounded up: Hi = fl(v1 + w1) >= v1 + w1 - ulp(Hi) / 2
+        enew = __builtin_fma(Hi - v1, 1.0 + 0x1p-50, 0x1p-50 * __builtin_fabs(Hi));
       } else {
         if (col) amb |= 1ull << j;
         a = v1 <= Ve ? i1 : ie;
         vnew = v1 <= Ve ? v1 : Ve;
         const double Lo = L1 < Ve ? L1 : Ve;
         enew = (H - Lo) * (1.0 + 0x1p-40) + 0x1p-50 * __builtin_fabs(vnew);
-        pnew = (j + 1) << 8;
       }
       if (col) {
         L.ag[j][lane] = (uint8_t)a;
@@ -362,8 +370,8 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
           if (k == j + 1) OPTa[k] = vnew;  // wave-uniform index
         if (exnew) exact |= 2ull << j;
         Emax = enew > Emax ? enew : Emax;
-        pv_prev = pv_cur;
-        pv_cur = pnew;
+        opt_jm1 = opt_j;
+        opt_j = vnew;
       }
     }
     // find_segments (utils.py:633-644): starts of the optimal segments + the last point
