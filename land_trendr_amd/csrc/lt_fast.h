@@ -32,7 +32,6 @@ __device__ inline int wave_max(int v) {
 template <int MAXY, class VT>
 struct WaveLds {
   VT ys[MAXY][64];       // present values (t), compacted in place to non-spike (k)
-  uint8_t sc[MAXY][64];  // scene slot of present point t
   uint8_t xn[MAXY][64];  // year offset of non-spike point k
   uint8_t ag[MAXY][64];  // DP argmin of column k; after the backtrack: non-spike index of vertex q
   int32_t year[LT_MAX_YEARS];  // the scene's calendar year per slot (64 words: one bank each)
@@ -56,6 +55,7 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
 
   // ---- pick_winners (utils.py:491-521) over wave-uniform year slots ----
   int T = 0, y0 = 0;
+  uint64_t pres = 0;  // year slots with a winner: present point t is the t-th set bit
   bool f32_bad = false;
   for (int y = 0; y < Y; y++) {
     int best = -1, bd = 0x7fffffff;
@@ -80,7 +80,7 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
         if (!((double)vs == v)) f32_bad = true;
       }
       L.ys[T][lane] = vs;
-      L.sc[T][lane] = (uint8_t)y;
+      pres |= 1ull << y;
       T++;
       if (out.val_raw) out.val_raw[q] = v;
     } else {
@@ -154,10 +154,14 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
       yv = zv;
     }
     // dropna: compact the non-spike points in place (k <= t)
+    uint64_t rem = pres;
     for (int t = 0; t < Tmax; t++) {
-      if (!(ok && t < T) || ((spike >> t) & 1)) continue;
+      if (!(ok && t < T)) continue;
+      const int y = __builtin_ctzll(rem);
+      rem &= rem - 1;
+      if ((spike >> t) & 1) continue;
       L.ys[n][lane] = L.ys[t][lane];
-      L.xn[n][lane] = (uint8_t)(L.year[L.sc[t][lane]] - y0);
+      L.xn[n][lane] = (uint8_t)(L.year[y] - y0);
       n++;
     }
   }
@@ -397,6 +401,7 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
   double prev_fit = 0.0;
   int32_t prev_year = 0;
   int ta = 0;                  // present index of vertex q (vertex 0 is the first point)
+  uint64_t wrem = pres;        // year slots of the present points from ta on
   for (int q = 0; q < nvmax; q++) {
     const bool act = q < nv;
     const int ka = act ? L.ag[q][lane] : 0;
@@ -435,7 +440,9 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
           continue;
         }
       }
-      const double x = (double)(L.year[L.sc[t][lane]] - y0);
+      const int y = __builtin_ctzll(wrem);
+      wrem &= wrem - 1;
+      const double x = (double)(L.year[y] - y0);
       double fv, fmv, fbv;
       if (s == 0 && q > 0 && !(pm == cm && pb == cb)) {
         const double fl = (pm * x) + pb;
@@ -451,7 +458,7 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
         fbv = cb;
       }
       if (s == 0) fit_vertex = fv;
-      const int64_t o = (int64_t)L.sc[t][lane] * os + p;
+      const int64_t o = (int64_t)y * os + p;
       if (out.val_fit) out.val_fit[o] = fv;
       if (out.fit_m) out.fit_m[o] = fmv;
       if (out.fit_b) out.fit_b[o] = fbv;
@@ -486,8 +493,8 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
   }
   if (!live || deferred) return !deferred;
   if (!ok) {  // the reference raises for this pixel: per-year fields of present years are NaN
-    for (int t = 0; t < T; t++) {
-      const int64_t o = (int64_t)L.sc[t][lane] * os + p;
+    for (uint64_t m = pres; m; m &= m - 1) {
+      const int64_t o = (int64_t)__builtin_ctzll(m) * os + p;
       if (out.val_fit) out.val_fit[o] = nan;
       if (out.fit_m) out.fit_m[o] = nan;
       if (out.fit_b) out.fit_b[o] = nan;

@@ -239,15 +239,10 @@ __host__ __device__ inline void dp_screened(int n, const uint8_t* xs, const doub
 template <int MAXY>
 __host__ __device__ inline bool dp_lazy(int n, const uint8_t* xs, const double* ys, double c,
                                         uint8_t* arg, uint64_t* amb_out = nullptr) {
-  // prov[k]: provenance of an inexact OPTa[k] = (base column << 8 | depth): the value is the
-  // base column's value with `depth` further "(0 + c) + ." steps applied. Equal provenance means
-  // the same operations on the same operand, i.e. bitwise-equal reference values.
   double OPTa[MAXY + 1], E[MAXY + 1];
-  uint16_t prov[MAXY + 1];
   uint64_t amb = 0;
   OPTa[0] = 0.0;
   E[0] = 0.0;
-  prov[0] = 0;
   for (int j = 0; j < n; j++) {
     double Sy = 0.0, Sxy = 0.0, Syy = 0.0;
     int Sx = 0, Sxx = 0;
@@ -257,8 +252,7 @@ __host__ __device__ inline bool dp_lazy(int n, const uint8_t* xs, const double* 
     const double inf = __builtin_inf();
     double Ve = inf;                   // min exact value; ie = first start attaining it
     double Hi = inf, Li1 = inf, Li2 = inf, vHi = 0.0, wHi = 0.0, vbest = inf;
-    int ie = -1, iHi = -1, ibest = -1;
-    int keyHi = -1, keyL1 = -2;
+    int ie = -1, iHi = -1, ibest = -1, iL1 = -2;
     for (int i = j; i >= 0; i--) {
       const int xi = xs[i];
       const double yi = ys[i];
@@ -291,21 +285,18 @@ __host__ __device__ inline bool dp_lazy(int n, const uint8_t* xs, const double* 
         continue;
       }
       w += 0x1p-50 * __builtin_fabs(v);
-      // candidates with equal keys have bitwise-equal reference values (and equal v, w)
-      const int key = m >= 3 ? 0x10000 | i : (int)prov[i] + 1;
       const double lo = v - w, hi = v + w;
       if (hi <= Hi) {
         Hi = hi;
         iHi = i;
-        keyHi = key;
         vHi = v;
         wHi = w;
       }
-      if (lo <= Li1) {
-        if (key != keyL1) Li2 = Li1;
+      if (lo <= Li1) {  // the two smallest lower ends (equal ones count twice)
+        Li2 = Li1;
         Li1 = lo;
-        keyL1 = key;
-      } else if (lo < Li2 && key != keyL1) {
+        iL1 = i;
+      } else if (lo < Li2) {
         Li2 = lo;
       }
     }
@@ -314,19 +305,16 @@ __host__ __device__ inline bool dp_lazy(int n, const uint8_t* xs, const double* 
       arg[j] = (uint8_t)ie;
       OPTa[j + 1] = Ve;
       E[j + 1] = 0.0;
-      prov[j + 1] = 0;
-    } else if (keyL1 == keyHi && Li2 > H && Ve > H) {  // one value lies below all others
+    } else if (iL1 == iHi && Li2 > H && Ve > H) {  // one start lies below all others
       arg[j] = (uint8_t)iHi;
       OPTa[j + 1] = vHi;
       E[j + 1] = wHi;
-      prov[j + 1] = keyHi >= 0x10000 ? (uint16_t)((j + 1) << 8) : (uint16_t)keyHi;
     } else {
       amb |= 1ull << j;
       arg[j] = (uint8_t)ibest;
       OPTa[j + 1] = vbest;
       const double L = Li1 < Ve ? Li1 : Ve;
       E[j + 1] = (H - L) * (1.0 + 0x1p-40) + 0x1p-50 * __builtin_fabs(vbest);
-      prov[j + 1] = (uint16_t)((j + 1) << 8);
     }
   }
   if (amb_out) *amb_out = amb;
