@@ -168,6 +168,87 @@ __host__ __device__ inline double nrm2(int n, G get) {
   return f80_sqrt_to_double(t);
 }
 
+// ------------------------------------------------------------------------------------------------
+// The same dnrm2 in binary64 pairs (the GPU's fp64 pipes instead of 64-bit integer emulation).
+// An extended value V is held as xdd{hi, lo}: V = hi + lo exactly, |lo| <= ulp53(hi) / 2, and V
+// has a 64-bit significand (lo is a multiple of ulp64(V)). Each x87 operation becomes an
+// error-free transformation (exact product / exact sum as a pair) followed by rounding the low
+// part to a multiple of ulp64(V) with round-half-even: (lo + C) - C with ulp(C) = ulp64(V). Since
+// hi is a multiple of 2^11 ulp64(V), the parity of the rounded low part is the parity of V's
+// 64-bit significand, so ties go the x87 way.
+// The sum is exact while the two exponents differ by <= 38 and the squares stay inside
+// [2^-900, 2^1000]; outside that `slow` is raised and the caller redoes the norm with nrm2().
+// ------------------------------------------------------------------------------------------------
+struct xdd {
+  double hi, lo;
+};
+
+// E with 2^E <= hi + lo < 2^(E+1) (hi > 0)
+__host__ __device__ inline int xdd_exp(double hi, double lo) {
+  int e;
+  const double mt = __builtin_frexp(hi, &e);  // hi = mt * 2^e, mt in [0.5, 1)
+  return (mt == 0.5 && lo < 0.0) ? e - 2 : e - 1;
+}
+
+// hi = RN(hi + lo), |lo| <= ulp53(hi) / 2: round hi + lo to a 64-bit significand (RNE)
+__host__ __device__ inline xdd xdd_round64(double hi, double lo) {
+  const double C = __builtin_ldexp(1.5, xdd_exp(hi, lo) - 11);  // ulp(C) = ulp64(hi + lo)
+  return xdd{hi, (lo + C) - C};
+}
+
+// x87 fmul of a double by itself
+__host__ __device__ inline xdd xdd_sq(double c, bool& slow) {
+  const double p = c * c;
+  const double e = __builtin_fma(c, c, -p);  // exact: c^2 = p + e
+  const double a = __builtin_fabs(c);
+  slow |= (a != 0.0 && a < 0x1p-450) || a > 0x1p500;
+  return xdd_round64(p, e);
+}
+
+// x87 fadd of two non-negative extended values
+__host__ __device__ inline xdd xdd_add(xdd A, xdd B, bool& slow) {
+  int ea, eb;
+  __builtin_frexp(A.hi, &ea);
+  __builtin_frexp(B.hi, &eb);
+  slow |= A.hi != 0.0 && B.hi != 0.0 && (ea - eb > 38 || eb - ea > 38);
+  const double s = A.hi + B.hi;  // TwoSum: A.hi + B.hi = s + t
+  const double bb = s - A.hi;
+  const double t = (A.hi - (s - bb)) + (B.hi - bb);
+  const double r = (t + A.lo) + B.lo;  // exact: all three are multiples of ulp64 of the smaller
+  const double s2 = s + r;             // TwoSum: s + r = s2 + r2
+  const double b2 = s2 - s;
+  const double r2 = (s - (s2 - b2)) + (r - b2);
+  return xdd_round64(s2, r2);
+}
+
+__host__ __device__ inline f80 xdd_to_f80(xdd v) {
+  if (v.hi == 0.0) return f80{0, 0};
+  const int E = xdd_exp(v.hi, v.lo);
+  // hi * 2^(63-E) is an integer in [2^63, 2^64]: scale by 2^(62-E), double in integers (2^64
+  // wraps to 0 and the negative low part brings it back)
+  const uint64_t h = (uint64_t)__builtin_ldexp(v.hi, 62 - E) << 1;
+  const int64_t l = (int64_t)__builtin_ldexp(v.lo, 63 - E);
+  return f80{h + (uint64_t)l, E};
+}
+
+// nrm2 (OpenBLAS dnrm2_k SkylakeX) on xdd accumulators; identical result unless `slow` is raised
+template <class G>
+__host__ __device__ inline double nrm2_dd(int n, G get, bool& slow) {
+  if (n <= 0) return 0.0;
+  if (n == 1) return __builtin_fabs(get(0));
+  xdd a0{0.0, 0.0}, a1{0.0, 0.0}, a2{0.0, 0.0}, a3{0.0, 0.0};
+  int n8 = n & ~7, j = 0;
+  for (; j < n8; j += 4) {
+    a0 = xdd_add(a0, xdd_sq(get(j), slow), slow);
+    a1 = xdd_add(a1, xdd_sq(get(j + 1), slow), slow);
+    a2 = xdd_add(a2, xdd_sq(get(j + 2), slow), slow);
+    a3 = xdd_add(a3, xdd_sq(get(j + 3), slow), slow);
+  }
+  for (; j < n; j++) a0 = xdd_add(a0, xdd_sq(get(j), slow), slow);
+  const xdd t = xdd_add(xdd_add(xdd_add(a0, a2, slow), a1, slow), a3, slow);
+  return f80_sqrt_to_double(xdd_to_f80(t));
+}
+
 // OpenBLAS dgemv_t SkylakeX, one column: sum_k a(k) v(k) with 4 interleaved lanes + FMA tail.
 template <class GA, class GV>
 __host__ __device__ inline double gemv_t1(int m, GA a, GV v) {
@@ -587,9 +668,11 @@ __host__ __device__ inline int lstsq_xint(int m, GX X, GY Y, bool need_solution,
     icpt = sI;
     return rank == 2 ? 0 : -3;
   }
-  // pass B: H2 on c[1:], ||c[2:]|| in soft-float80
+  // pass B: H2 on c[1:], ||c[2:]|| in binary64 pairs (soft-float80 on the rare fallback)
   const double r12 = C(0), alpha2 = C(1);
-  const double xn2 = nrm2(m - 2, [&](int k) { return C(k + 2); });
+  bool slow = false;
+  double xn2 = nrm2_dd(m - 2, [&](int k) { return C(k + 2); }, slow);
+  if (slow) xn2 = nrm2(m - 2, [&](int k) { return C(k + 2); });
   double tau2 = 0.0, beta2 = alpha2, s2 = 0.0;
   if (xn2 != 0.0) {
     beta2 = -__builtin_copysign(dlapy2(alpha2, xn2), alpha2);

@@ -69,3 +69,11 @@ extern "C" int ltx_lstsq_xint(int m, const double* x, const double* y, int need_
   out3[2] = r;
   return rc;
 }
+
+// dnrm2 on binary64 pairs; *slow = 1 when the caller would fall back to nrm2()
+extern "C" double ltx_nrm2_dd(int n, const double* x, int* slow) {
+  bool s = false;
+  const double r = lt::nrm2_dd(n, [&](int k) { return x[k]; }, s);
+  *slow = s;
+  return r;
+}

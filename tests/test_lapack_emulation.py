@@ -128,3 +128,46 @@ def test_integer_x_fused_variant_matches_oracle(hc):
             if ssr:
                 bad += not golden_io._bits_equal(o[2], want[3])
     assert bad == 0
+
+
+def test_pair_arithmetic_nrm2_matches_integer_f80(hc):
+    """nrm2_dd (binary64 pairs) is bit-identical to the integer soft-float80 nrm2 whenever it does
+    not ask for the fallback; adversarial inputs: squares on binade edges (c = 2^k (1 +- eps)),
+    exact ties of the 64-bit rounding, zeros, wide exponent spreads."""
+    L = hc
+    L.ltx_nrm2_dd.argtypes = [ctypes.c_int, D, ctypes.POINTER(ctypes.c_int)]
+    L.ltx_nrm2_dd.restype = ctypes.c_double
+    rng = np.random.default_rng(99)
+    slow = ctypes.c_int(0)
+    bad = 0
+    nslow = [0] * 6
+    for t in range(40000):
+        n = int(rng.integers(1, 66))
+        kind = t % 6
+        if kind == 0:
+            x = rng.normal(0, 1, n)
+        elif kind == 1:
+            x = rng.normal(0, 1, n) * 10.0 ** rng.integers(-12, 12, n)
+        elif kind == 2:  # near powers of two: c^2 rounds onto / just below a binade edge
+            k = rng.integers(-4, 5, n).astype(np.float64)
+            eps = rng.integers(-3, 4, n) * 2.0 ** -52
+            x = np.ldexp(1.0 + eps, k.astype(int)) * np.where(rng.random(n) < 0.5, -1, 1)
+        elif kind == 3:  # 27-bit significands: squares exact in 54 bits, sums with exact ties
+            x = np.ldexp(rng.integers(1 << 26, 1 << 27, n).astype(np.float64),
+                         rng.integers(-6, 1, n))
+        elif kind == 4:  # zeros and repeated values
+            x = rng.choice([0.0, 1.0, -1.0, 3.0, 0.5, 1e-3], n)
+        else:  # what the fit sees: c = 1 + sc * x * s1 over increasing integer x
+            xs = np.sort(rng.choice(np.arange(0, 70), n, replace=False)).astype(np.float64)
+            s1 = 1.0 / (xs[0] - np.sqrt(xs[0] ** 2 + (xs[1:] ** 2).sum() if n > 1 else 1.0))
+            x = 1.0 + rng.normal(-1, 0.5) * xs * s1
+        x = np.ascontiguousarray(x, np.float64)
+        want = hc.ltx_nrm2(n, x.ctypes.data_as(D))
+        got = hc.ltx_nrm2_dd(n, x.ctypes.data_as(D), ctypes.byref(slow))
+        if slow.value:
+            nslow[kind] += 1
+            continue
+        bad += not golden_io._bits_equal(got, want)
+    assert bad == 0
+    print('fallbacks per kind (of %d):' % (40000 // 6), nslow)
+    assert nslow[0] + nslow[2] + nslow[3] + nslow[4] + nslow[5] < 40000 // 6 * 0.05
