@@ -13,6 +13,11 @@
 #pragma once
 #include "lt_pixel.h"
 
+// Diagnostic builds only (never the product): LT_ABLATE=1 skips the vertex fits, 2 the DP.
+#ifndef LT_ABLATE
+#define LT_ABLATE 0
+#endif
+
 namespace lt {
 
 // max over the 64 lanes of a wave (every lane must call it). readfirstlane makes the result an
@@ -264,7 +269,7 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
         j = a - 1;
       }
     }
-  } else if (nmax >= 1) {
+  } else if (nmax >= 1 && LT_ABLATE != 2) {
     const double c = P.line_cost;
     const double inf = __builtin_inf();
     double OPTa[MAXY + 1];
@@ -413,7 +418,7 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
     const int mseg = has_next ? kb - ka + 1 : 2;
     const int kbase = has_next ? ka : 0;
     double sm = 0.0, sbv = 0.0, ssr = 0.0;
-    if (__ballot(has_next)) {
+    if (LT_ABLATE != 1 && __ballot(has_next)) {
       const int rc = lstsq_xint(
           mseg, [&](int k) { return has_next ? (int)L.xn[kbase + k][lane] : k; },
           [&](int k) { return has_next ? (double)L.ys[kbase + k][lane] : 0.0; }, true, false,

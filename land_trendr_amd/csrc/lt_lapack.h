@@ -231,6 +231,30 @@ __host__ __device__ inline f80 xdd_to_f80(xdd v) {
   return f80{h + (uint64_t)l, E};
 }
 
+// (double) sqrtl(V) — x87 fsqrt (RN to 64 bits) then the store to binary64 (RN to 53 bits) — for
+// V = hi + lo as above, in binary64: s = sqrt(hi), d ~ (V - s^2) / 2s from the exact remainder,
+// so sqrt(V) = s + d to ~2^-100 relative. The 64-bit rounding is k = round(d / ulp64) (sqrt(V)
+// is never a 64-bit midpoint; within 2^-20 ulp64 of one `slow` is raised), the 53-bit rounding of
+// s + k ulp64 is integer work on k. s a power of two with d < 0 (a binade edge) raises `slow`.
+__host__ __device__ inline double xdd_sqrt_to_double(double hi, double lo, bool& slow) {
+  if (hi == 0.0) return 0.0;
+  const double s = __builtin_sqrt(hi);
+  const double e1 = __builtin_fma(-s, s, hi);  // hi - s^2, exact for a correctly rounded s
+  const double d = (e1 + lo) / (2.0 * s);
+  int E;
+  const double mt = __builtin_frexp(s, &E);  // s in [2^(E-1), 2^E): ulp53 = 2^(E-53)
+  const double kd = __builtin_ldexp(d, 64 - E);  // d in units of ulp64 = 2^(E-64)
+  const double kf = __builtin_floor(kd);
+  slow |= (mt == 0.5 && d < 0.0) || __builtin_fabs(kd - kf - 0.5) < 0x1p-20 ||
+          __builtin_fabs(kd) > 0x1p13;
+  const int k = (int)kf + (kd - kf > 0.5 ? 1 : 0);  // RN(sqrt V) to 64 bits = s + k ulp64
+  int a = k >> 11;                                  // s + a ulp53 <= q64 < s + (a+1) ulp53
+  const int b = k - (a << 11);
+  const int odd = (int)((dbl_bits(s) + (uint64_t)(int64_t)a) & 1);
+  if (b > 1024 || (b == 1024 && odd)) a++;
+  return s + __builtin_ldexp((double)a, E - 53);
+}
+
 // nrm2 (OpenBLAS dnrm2_k SkylakeX) on xdd accumulators; identical result unless `slow` is raised
 template <class G>
 __host__ __device__ inline double nrm2_dd(int n, G get, bool& slow) {
@@ -246,7 +270,7 @@ __host__ __device__ inline double nrm2_dd(int n, G get, bool& slow) {
   }
   for (; j < n; j++) a0 = xdd_add(a0, xdd_sq(get(j), slow), slow);
   const xdd t = xdd_add(xdd_add(xdd_add(a0, a2, slow), a1, slow), a3, slow);
-  return f80_sqrt_to_double(xdd_to_f80(t));
+  return xdd_sqrt_to_double(t.hi, t.lo, slow);
 }
 
 // OpenBLAS dgemv_t SkylakeX, one column: sum_k a(k) v(k) with 4 interleaved lanes + FMA tail.
@@ -600,7 +624,12 @@ __host__ __device__ inline int lstsq_xint(int m, GX X, GY Y, bool need_solution,
     S += (uint64_t)((int64_t)xk * xk);
   }
   const double alpha = (double)x0;
-  const double xn = m == 2 ? (double)X(1) : f80_sqrt_to_double(f80_from_u64(S));
+  double xn = (double)X(1);
+  if (m > 2) {
+    bool slow = S >= (1ull << 53);
+    xn = xdd_sqrt_to_double((double)S, 0.0, slow);
+    if (slow) xn = f80_sqrt_to_double(f80_from_u64(S));
+  }
   const double beta1 = -__builtin_copysign(dlapy2(alpha, xn), alpha);  // xn > 0
   const double tau1 = (beta1 - alpha) / beta1;
   const double s1 = 1.0 / (alpha - beta1);

@@ -77,3 +77,11 @@ extern "C" double ltx_nrm2_dd(int n, const double* x, int* slow) {
   *slow = s;
   return r;
 }
+
+// x87 sqrt-then-store of hi + lo: out2 = {binary64 path, integer soft-float80 path}; returns slow
+extern "C" int ltx_sqrt_pair(double hi, double lo, double* out2) {
+  bool s = false;
+  out2[0] = lt::xdd_sqrt_to_double(hi, lo, s);
+  out2[1] = lt::f80_sqrt_to_double(lt::xdd_to_f80(lt::xdd{hi, lo}));
+  return s;
+}

@@ -171,3 +171,55 @@ def test_pair_arithmetic_nrm2_matches_integer_f80(hc):
     assert bad == 0
     print('fallbacks per kind (of %d):' % (40000 // 6), nslow)
     assert nslow[0] + nslow[2] + nslow[3] + nslow[4] + nslow[5] < 40000 // 6 * 0.05
+
+
+def _round64(v):
+    """Fraction -> nearest value with a 64-bit significand (ties to even), as a Fraction."""
+    from fractions import Fraction
+    if v == 0:
+        return Fraction(0)
+    e = v.numerator.bit_length() - v.denominator.bit_length()
+    while Fraction(2) ** e > v:
+        e -= 1
+    while Fraction(2) ** (e + 1) <= v:
+        e += 1
+    u = Fraction(2) ** (e - 63)
+    q, r = divmod(v, u)
+    if r * 2 > u or (r * 2 == u and q % 2 == 1):
+        q += 1
+    return q * u
+
+
+def test_pair_sqrt_matches_integer_f80(hc):
+    """xdd_sqrt_to_double: x87 double rounding of sqrt (64 then 53 bits) on pairs, against the
+    integer soft-float80 path, including values whose root sits next to a 53-bit midpoint."""
+    from fractions import Fraction
+    hc.ltx_sqrt_pair.argtypes = [ctypes.c_double, ctypes.c_double, D]
+    rng = np.random.default_rng(2718)
+    out = (ctypes.c_double * 2)()
+    bad = nslow = 0
+    N = 20000
+    for t in range(N):
+        kind = t % 3
+        if kind == 0:  # random 64-bit significand
+            sig = int(rng.integers(1 << 62, 1 << 63)) * 2 + int(rng.integers(0, 2))
+            V = Fraction(sig) * Fraction(2) ** int(rng.integers(-80, 80))
+        elif kind == 1:  # root next to a 53-bit midpoint: (M + 1/2 + delta)^2, rounded to 64 bits
+            M = int(rng.integers(1 << 52, 1 << 53))
+            delta = Fraction(int(rng.integers(-64, 65)), 1 << int(rng.integers(10, 40)))
+            V = _round64((Fraction(M) + Fraction(1, 2) + delta) ** 2)
+            V *= Fraction(2) ** (2 * int(rng.integers(-40, 10)))
+        else:  # perfect squares and small integers (the x-norm case)
+            V = Fraction(int(rng.integers(1, 1 << 40)))
+            if t % 2:
+                r = int(rng.integers(1, 1 << 26))
+                V = Fraction(r * r)
+        hi = float(V)
+        lo = float(V - Fraction(hi))
+        slow = hc.ltx_sqrt_pair(hi, lo, ctypes.cast(out, D))
+        if slow:
+            nslow += 1
+            continue
+        bad += not golden_io._bits_equal(out[0], out[1])
+    assert bad == 0
+    assert nslow < N * 0.01
