@@ -62,22 +62,47 @@ __global__ __launch_bounds__(64) void analyze_fast_kernel(const lt::DevScene* __
 }
 
 // Stage 2 (wave-lockstep, lt_fast.h with EXACT): the deferred pixels, binary64 series in LDS,
-// exact-OPT DP. A fixed grid strides over the list in whole waves.
+// exact-OPT DP. A grid of exactly the resident waves takes 64-pixel groups of the list from a
+// counter (group cost varies a lot); every wave leaves once the counter has passed the list.
 template <int MAXY, int RMAX>
 __global__ __launch_bounds__(64) void resolve_fast_kernel(const lt::DevScene* __restrict__ S,
                                                           const lt_params P, const lt_tile_in in,
                                                           const lt_tile_out out,
                                                           const int64_t* __restrict__ defer,
-                                                          const unsigned long long* __restrict__ n_defer) {
+                                                          unsigned long long* __restrict__ counters) {
   __shared__ lt::WaveLds<MAXY, double> L;
   const int lane = threadIdx.x;
-  const int64_t n = (int64_t)*n_defer;
-  for (int64_t base = (int64_t)blockIdx.x * 64; base < n; base += (int64_t)gridDim.x * 64) {
+  const int64_t n = (int64_t)counters[0];  // written by stage 1, a previous launch
+  for (;;) {
+    unsigned g = 0;
+    if (lane == 0) g = atomicAdd((unsigned*)&counters[1], 1u);
+    g = __builtin_amdgcn_readfirstlane(__shfl(g, 0));
+    const int64_t base = (int64_t)g * 64;
+    if (base >= n) break;
     const int64_t k = base + lane;
     const bool live = k < n;
     lt::analyze_fast<MAXY, RMAX, true, double>(*S, P, in, out, live ? defer[k] : 0, live, lane,
                                                L);
   }
+}
+
+// waves of resolve_fast_kernel<MAXY, RMAX> the device holds at once
+template <int MAXY, int RMAX>
+static unsigned resolve_grid(int device) {
+  static int cached_dev = -1;
+  static unsigned cached = 0;
+  if (cached_dev != device) {
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, resolve_fast_kernel<MAXY, RMAX>, 64,
+                                                     0) != hipSuccess || per_cu < 1)
+      per_cu = 1;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
+        cus < 1)
+      cus = 256;
+    cached = (unsigned)(per_cu * cus);
+    cached_dev = device;
+  }
+  return cached;
 }
 
 // Stage 2 (per-lane reference body, lt_pixel.h): kept for the host harness's structure.
@@ -269,10 +294,12 @@ int lt_analyze_tile(lt_ctx* c, const lt_scene* sc, const lt_params* prm, const l
     if (c->d_defer) HIP_OR_FAIL(c, hipFree(c->d_defer));
     c->d_defer = nullptr;
     HIP_OR_FAIL(c, hipMalloc((void**)&c->d_defer, sizeof(int64_t) * (size_t)in->n_pix));
-    if (!c->d_ndefer) HIP_OR_FAIL(c, hipMalloc((void**)&c->d_ndefer, sizeof(unsigned long long)));
+    if (!c->d_ndefer)
+      HIP_OR_FAIL(c, hipMalloc((void**)&c->d_ndefer, 2 * sizeof(unsigned long long)));
     c->defer_cap = in->n_pix;
   }
-  HIP_OR_FAIL(c, hipMemsetAsync(c->d_ndefer, 0, sizeof(unsigned long long), stream));
+  // [0]: deferred-pixel count (stage 1), [1]: the resolve stage's work counter
+  HIP_OR_FAIL(c, hipMemsetAsync(c->d_ndefer, 0, 2 * sizeof(unsigned long long), stream));
 
   EventPair* ep[2] = {nullptr, nullptr};
   if (c->timing) {
@@ -304,10 +331,13 @@ int lt_analyze_tile(lt_ctx* c, const lt_scene* sc, const lt_params* prm, const l
   HIP_OR_FAIL(c, hipGetLastError());
   if (ep[0]) HIP_OR_FAIL(c, hipEventRecord(ep[0]->stop, stream));
   if (ep[1]) HIP_OR_FAIL(c, hipEventRecord(ep[1]->start, stream));
-  dim3 rg((unsigned)(nwave < 1536 ? nwave : 1536));
 #define LT_LAUNCH_RESOLVE(MY, RM)                                                            \
-  hipLaunchKernelGGL((resolve_fast_kernel<MY, RM>), rg, fblock, 0, stream, c->d_scene, *prm, \
-                     *in, *out, c->d_defer, c->d_ndefer)
+  do {                                                                                      \
+    const unsigned g = resolve_grid<MY, RM>(c->device);                                     \
+    dim3 rg((unsigned)(nwave < (int64_t)g ? nwave : (int64_t)g));                           \
+    hipLaunchKernelGGL((resolve_fast_kernel<MY, RM>), rg, fblock, 0, stream, c->d_scene,    \
+                       *prm, *in, *out, c->d_defer, c->d_ndefer);                           \
+  } while (0)
   if (Y <= 32) {
     if (few) LT_LAUNCH_RESOLVE(32, 4); else LT_LAUNCH_RESOLVE(32, 16);
   } else if (Y <= 48) {
