@@ -278,6 +278,8 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
     uint64_t exact = 1;      // bit k: OPTa[k] is the reference value itself
     double Emax = 0.0;       // bound on |OPTa[k] - OPT[k]| for every inexact k so far
     double opt_j = 0.0, opt_jm1 = 0.0;  // OPTa[j] and OPTa[j-1] (the 1- and 2-point starts)
+    double SyyAll = 0.0;                // sum of y^2 over the points 0..j
+    const bool prune = c >= 0.0;
     uint64_t amb = 0;
     for (int jj = 0; jj < nmax; jj++) {
       const int j = __builtin_amdgcn_readfirstlane(jj);  // column index in an SGPR
@@ -288,6 +290,38 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
       // lower ends (L1 at start iL, L2); Ve/ie: the exact candidates
       double Ve = inf, Hi = inf, L1 = inf, L2 = inf, v1 = inf;
       int ie = 0, i1 = 0, iL = -1;
+      // starts in decreasing order ("<=" keeps the smaller start among equal values). First the
+      // 1- and 2-point starts: residual exactly 0, so with an exact OPTa the value is the
+      // reference's own; otherwise an interval of half-width Emax + rounding.
+#pragma unroll
+      for (int s = 0; s <= 1; s++) {
+        const int i = j - s;
+        if (i < 0) continue;  // wave-uniform
+        const double v = c + (s ? opt_jm1 : opt_j);
+        if ((exact >> i) & 1) {
+          if (v <= Ve) {
+            Ve = v;
+            ie = i;
+          }
+        } else {
+          const double w = __builtin_fma(0x1p-50, __builtin_fabs(v), Emax);
+          const double hi = v + w, lo = v - w;
+          if (hi <= Hi) {
+            i1 = i;
+            v1 = v;
+          }
+          Hi = hi <= Hi ? hi : Hi;
+          const bool bl = lo <= L1;
+          L2 = bl ? L1 : (lo < L2 ? lo : L2);
+          L1 = bl ? lo : L1;
+          iL = bl ? i : iL;
+        }
+      }
+      // prefix bound for the early exit below: every segment ending at j has Syy <= SyyAll
+      {
+        const double yj = (double)L.ys[j][lane];
+        SyyAll = __builtin_fma(yj, yj, SyyAll);
+      }
 #pragma unroll
       for (int i = MAXY - 1; i >= 0; i--) {
         if (i > j) continue;  // wave-uniform
@@ -298,7 +332,7 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
         Sy += yi;
         Sxy = __builtin_fma((double)xi, yi, Sxy);
         Syy = __builtin_fma(yi, yi, Syy);
-        if (i + 2 > j) continue;  // the 1- and 2-point starts are priced after the loop
+        if (i + 2 > j) continue;  // the 1- and 2-point starts are priced above
         // closed-form SSE: (m*Syy - Sy^2 - N1^2/D) / m, one reciprocal
         const int m = j - i + 1;  // wave-uniform, >= 3
         const double md = (double)m;
@@ -315,7 +349,7 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
         const double wopt = ((exact >> i) & 1) ? 0.0 : Emax;
         const double w = __builtin_fma(0x1p-50, __builtin_fabs(v), __builtin_fma(kScreen, Syy, wopt));
         const double hi = v + w, lo = v - w;
-        if (hi <= Hi) {  // i descends: "<=" keeps the smaller start among equal upper ends
+        if (hi <= Hi) {
           i1 = i;
           v1 = v;
         }
@@ -324,32 +358,14 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
         L2 = bl ? L1 : (lo < L2 ? lo : L2);
         L1 = bl ? lo : L1;
         iL = bl ? i : iL;
-      }
-      // the 2-point then the 1-point start (larger starts than every start above: strict "<"
-      // keeps the first minimum). Their residuals are exactly 0, so with an exact OPTa the
-      // value is the reference's own; otherwise an interval of half-width Emax + rounding.
-#pragma unroll
-      for (int s = 1; s >= 0; s--) {
-        const int i = j - s;
-        if (i < 0) continue;  // wave-uniform
-        const double v = c + (s ? opt_jm1 : opt_j);
-        if ((exact >> i) & 1) {
-          if (v < Ve) {
-            Ve = v;
-            ie = i;
-          }
-        } else {
-          const double w = __builtin_fma(0x1p-50, __builtin_fabs(v), Emax);
-          const double hi = v + w, lo = v - w;
-          if (hi < Hi) {
-            i1 = i;
-            v1 = v;
-          }
-          Hi = hi < Hi ? hi : Hi;
-          const bool bl = lo <= L1;
-          L2 = bl ? L1 : (lo < L2 ? lo : L2);
-          L1 = bl ? lo : L1;
-          iL = bl ? i : iL;
+        // early exit: a longer segment has a residual at least this one's (least squares on a
+        // superset of the points), OPT >= 0 (line_cost >= 0), so every start below i is worth
+        // at least lb: once lb exceeds the best upper end so far in every lane, none of them
+        // can be the minimum (or tie it), nor move a lower end that the decision reads
+        if (prune) {
+          const double lb = (__builtin_fma(-2.0 * kScreen, SyyAll, e) + c) * (1.0 - 0x1p-50);
+          const double Hb = Hi < Ve ? Hi : Ve;
+          if (!__ballot(col && !(lb > Hb))) break;
         }
       }
       const double H = Hi < Ve ? Hi : Ve;  // the exact minimum lies in [min(L1, Ve), H]
