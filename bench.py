@@ -62,6 +62,21 @@ def bytes_per_pixel(cfg, n_obs, n_years):
     return inp + lab + tl + 4                                     # + status
 
 
+PMC_SUMMARY = os.path.join(ROOT, 'profiles', 'r01_pmc_c2.json')
+
+
+def pmc_traffic(kernel, px_per_launch):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc summary of this build
+    (FETCH_SIZE/WRITE_SIZE passes, gfx950-corrected: profiles/summarize_pmc.py), scaled to this
+    launch's pixel count; None when absent."""
+    try:
+        with open(PMC_SUMMARY) as f:
+            d = json.load(f)
+        return d[kernel]['hbm_bytes'] / d['_pixels_per_launch'] * px_per_launch
+    except (OSError, KeyError, ValueError, TypeError, ZeroDivisionError):
+        return None
+
+
 def cpu_baseline(cfg, seconds):
     """The oracle (C restatement, pthreads over all host cores) on a bounded sample."""
     from oracle import oracle
@@ -177,6 +192,9 @@ def main():
     px_per_launch = P * args.steps / n_launch
     flops = f_ref(cfg['years']) * px_per_launch
     achieved = flops / (kern_ms * 1e-3) / 1e12
+    bpp = bytes_per_pixel(cfg, meta.n_obs, meta.n_years)
+    hbm_gbs = bpp * px_per_launch / (kern_ms * 1e-3) / 1e9
+    traffic = pmc_traffic('analyze', px_per_launch) if args.config == 'c2' else None
     res = {
         'metric': 'Mpixels/sec full analyze (30-yr series)' if cfg['years'] == 30 else
                   'Mpixels/sec full analyze (%d-yr series)' % cfg['years'],
@@ -188,14 +206,20 @@ def main():
                    'obs': meta.n_obs, 'rules': len(rules), 'line_cost': cfg['line_cost'],
                    'tile_pixels': args.tile, 'gather': bool(gather),
                    'parallelism': 'pixel tiles, 1 scene per GPU'},
+        # dominant kernel: the analyze stage, FP64-VALU bound (O(n^2) DP per 240-byte series).
+        # achieved = the reference algorithm's flops (F_ref) per launch / the
+        # launch's HIP-event time: frac > 1 means faster than the reference's own arithmetic could
+        # run at FP64 peak (the kernel proves most candidate fits irrelevant)
         'roofline': {'bound': 'fp64-valu', 'achieved': round(achieved, 3),
                      'peak': FP64_PEAK_TFLOPS, 'unit': 'TFLOP/s',
-                     'frac': round(achieved / FP64_PEAK_TFLOPS, 4), 'traffic': None,
-                     'kernel': 'analyze_kernel', 'kernel_ms': round(kern_ms, 3),
-                     'flops_per_px': f_ref(cfg['years']),
-                     'algorithmic_bytes_per_px': bytes_per_pixel(cfg, meta.n_obs, meta.n_years),
-                     'hbm_gbs_algorithmic': round(bytes_per_pixel(cfg, meta.n_obs, meta.n_years)
-                                                  * px_per_launch / (kern_ms * 1e-3) / 1e9, 2)},
+                     'frac': round(achieved / FP64_PEAK_TFLOPS, 4),
+                     'traffic': None if traffic is None else round(traffic),
+                     'traffic_source': os.path.relpath(PMC_SUMMARY, ROOT) if traffic else None,
+                     'kernel': 'analyze_fast_kernel', 'kernel_ms': round(kern_ms, 3),
+                     'flops_per_px': f_ref(cfg['years']), 'flops_model': 'F_ref (SURVEY.md 8(d))',
+                     'algorithmic_bytes_per_px': bpp,
+                     'hbm': {'achieved': round(hbm_gbs, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                             'frac': round(hbm_gbs / HBM_PEAK_GBS, 4)}},
         'status_numeric_pixels': n_numeric,
         'resolve_stage': {'ms_per_launch': round(resolve_ms, 3),
                           'deferred_pixels_last_tile': n_deferred_last,

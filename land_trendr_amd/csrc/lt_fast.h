@@ -184,12 +184,19 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
     double lo[MAXY];
 #pragma unroll
     for (int k = 0; k <= MAXY; k++) OPT[k] = 0.0;
+    double SyyAll = 0.0;  // sum of y^2 over the points 0..j (early-exit bound, as below)
+    const bool prune = c >= 0.0;
     for (int jj = 0; jj < nmax; jj++) {
       const int j = __builtin_amdgcn_readfirstlane(jj);
       const bool col = j < n;
       double Sy = 0.0, Sxy = 0.0, Syy = 0.0;
       int Sx = 0, Sxx = 0;
       double H = inf;
+      int imin = 0;  // starts below imin were never priced (early exit)
+      {
+        const double yj = (double)L.ys[j][lane];
+        SyyAll = __builtin_fma(yj, yj, SyyAll);
+      }
 #pragma unroll
       for (int i = MAXY - 1; i >= 0; i--) {
         if (i > j) continue;  // wave-uniform
@@ -217,11 +224,17 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
         if (m >= 3) w = __builtin_fma(0x1p-50, __builtin_fabs(v), kScreen * Syy);
         lo[i] = v - w;
         H = v + w < H ? v + w : H;
+        // early exit (same argument as the lazy DP): no start below i can reach H
+        if (prune && m >= 3) {
+          imin = i;
+          const double lb = (__builtin_fma(-2.0 * kScreen, SyyAll, e) + c) * (1.0 - 0x1p-50);
+          if (!__ballot(col && !(lb > H))) break;
+        }
       }
       uint64_t cand = 0;  // starts whose interval reaches H: the exact minimum is among them
 #pragma unroll
       for (int i = 0; i < MAXY; i++)
-        if (i <= j && lo[i] <= H) cand |= 1ull << i;
+        if (i <= j && i >= imin && lo[i] <= H) cand |= 1ull << i;
       const int nc = col ? __builtin_popcountll(cand) : 0;
       const int ncmax = wave_max(nc);
       double best = inf;

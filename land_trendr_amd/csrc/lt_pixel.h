@@ -172,11 +172,14 @@ template <int MAXY>
 __host__ __device__ inline void dp_screened(int n, const uint8_t* xs, const double* ys, double c,
                                    double* OPT, uint8_t* arg, int& status) {
   double va[MAXY];
+  double SyyAll = 0.0;  // sum of y^2 over the points 0..j
   for (int j = 0; j < n; j++) {
     // pass 1: approximate price of every start, i from j down to 0 (incremental sums)
     double Sy = 0.0, Sxy = 0.0, Syy = 0.0;
     int Sx = 0, Sxx = 0;
-    double vmin = __builtin_inf(), wmax = 0.0;
+    double vmin = __builtin_inf(), wmax = 0.0, Hc = __builtin_inf();
+    SyyAll += ys[j] * ys[j];
+    for (int i = 0; i <= j; i++) va[i] = __builtin_inf();
     for (int i = j; i >= 0; i--) {
       const int xi = xs[i];
       const double yi = ys[i];
@@ -201,6 +204,11 @@ __host__ __device__ inline void dp_screened(int n, const uint8_t* xs, const doub
       va[i] = v;
       vmin = v < vmin ? v : vmin;
       wmax = w > wmax ? w : wmax;
+      Hc = v + w < Hc ? v + w : Hc;
+      // early exit: a longer segment's residual is at least this one's (least squares on a
+      // superset), OPT >= 0 for line_cost >= 0, so every start below i is worth at least lb;
+      // lb > Hc >= the column minimum: none of them can be (or tie) the minimum
+      if (m >= 3 && c >= 0.0 && (e - 2.0 * kScreen * SyyAll + c) * (1.0 - 0x1p-50) > Hc) break;
     }
     // pass 2: exact price for the starts inside the window, first exact minimum wins
     const double lim = vmin + 2.0 * wmax;
@@ -243,7 +251,9 @@ __host__ __device__ inline bool dp_lazy(int n, const uint8_t* xs, const double* 
   uint64_t amb = 0;
   OPTa[0] = 0.0;
   E[0] = 0.0;
+  double SyyAll = 0.0;  // sum of y^2 over the points 0..j (early exit, as in dp_screened)
   for (int j = 0; j < n; j++) {
+    SyyAll += ys[j] * ys[j];
     double Sy = 0.0, Sxy = 0.0, Syy = 0.0;
     int Sx = 0, Sxx = 0;
     // Exact candidates (1-2 point segment: residual exactly 0, on an exact OPT) are computed
@@ -299,6 +309,8 @@ __host__ __device__ inline bool dp_lazy(int n, const uint8_t* xs, const double* 
       } else if (lo < Li2) {
         Li2 = lo;
       }
+      const double Hc = Hi < Ve ? Hi : Ve;
+      if (m >= 3 && c >= 0.0 && (e - 2.0 * kScreen * SyyAll + c) * (1.0 - 0x1p-50) > Hc) break;
     }
     const double H = Hi < Ve ? Hi : Ve;  // the exact minimum lies in [min lower bound, H]
     if (Li1 > H) {  // no interval reaches H: the exact candidates decide, bit-exactly
