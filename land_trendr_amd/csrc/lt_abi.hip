@@ -44,6 +44,7 @@ template <int MAXY, int RMAX>
 __global__ __launch_bounds__(64) void analyze_fast_kernel(const lt::DevScene* __restrict__ S,
                                                           const lt_params P, const lt_tile_in in,
                                                           const lt_tile_out out,
+                                                          const lt::lsq_xf* __restrict__ xtab,
                                                           int64_t* __restrict__ defer,
                                                           unsigned long long* __restrict__ n_defer) {
   __shared__ lt::WaveLds<MAXY, float> L;
@@ -51,7 +52,7 @@ __global__ __launch_bounds__(64) void analyze_fast_kernel(const lt::DevScene* __
   const int64_t p = (int64_t)blockIdx.x * 64 + lane;
   const bool live = p < in.n_pix;
   const bool deferred =
-      !lt::analyze_fast<MAXY, RMAX, false, float>(*S, P, in, out, p, live, lane, L) && live;
+      !lt::analyze_fast<MAXY, RMAX, false, float>(*S, P, in, out, xtab, p, live, lane, L) && live;
   const uint64_t mask = __ballot(deferred);
   if (mask == 0) return;
   const int leader = __ffsll((long long)mask) - 1;
@@ -68,6 +69,7 @@ template <int MAXY, int RMAX>
 __global__ __launch_bounds__(64) void resolve_fast_kernel(const lt::DevScene* __restrict__ S,
                                                           const lt_params P, const lt_tile_in in,
                                                           const lt_tile_out out,
+                                                          const lt::lsq_xf* __restrict__ xtab,
                                                           const int64_t* __restrict__ defer,
                                                           unsigned long long* __restrict__ counters) {
   __shared__ lt::WaveLds<MAXY, double> L;
@@ -81,9 +83,23 @@ __global__ __launch_bounds__(64) void resolve_fast_kernel(const lt::DevScene* __
     if (base >= n) break;
     const int64_t k = base + lane;
     const bool live = k < n;
-    lt::analyze_fast<MAXY, RMAX, true, double>(*S, P, in, out, live ? defer[k] : 0, live, lane,
-                                               L);
+    lt::analyze_fast<MAXY, RMAX, true, double>(*S, P, in, out, xtab, live ? defer[k] : 0, live,
+                                               lane, L);
   }
+}
+
+// one lsq_factor per slot of the x-set table (lt_lapack.h), computed by the device arithmetic
+// that the lookups replace
+__global__ __launch_bounds__(kBlock) void build_xtable_kernel(lt::lsq_xf* __restrict__ xtab) {
+  const int idx = blockIdx.x * kBlock + threadIdx.x;
+  if (idx >= lt::kXtSize) return;
+  int m = 0, xs[64];
+  lt::lsq_xf f{};
+  if (lt::xset_of_key(idx, m, xs))
+    lt::lsq_factor(m, [&](int k) { return xs[k]; }, f);
+  else
+    f.rc = -4;  // no x-set maps here
+  xtab[idx] = f;
 }
 
 // waves of resolve_fast_kernel<MAXY, RMAX> the device holds at once
@@ -150,6 +166,7 @@ struct lt_ctx {
   int64_t* d_defer = nullptr;    // deferred-pixel list of the resolve stage
   unsigned long long* d_ndefer = nullptr;
   int64_t defer_cap = 0;
+  lt::lsq_xf* d_xtab = nullptr;  // x-set factor table (built at context creation)
 };
 
 static int fail(lt_ctx* c, int code, const char* fmt, const char* detail = "") {
@@ -181,6 +198,13 @@ int lt_ctx_create(int device, lt_ctx** out) {
   if (e == hipSuccess) e = hipHostMalloc((void**)&c->h_scene, sizeof(lt::DevScene));
   if (e == hipSuccess) e = hipMalloc((void**)&c->d_scene, sizeof(lt::DevScene));
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->scene_copied, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipMalloc((void**)&c->d_xtab, sizeof(lt::lsq_xf) * lt::kXtSize);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(build_xtable_kernel, dim3((lt::kXtSize + kBlock - 1) / kBlock),
+                       dim3(kBlock), 0, 0, c->d_xtab);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipDeviceSynchronize();
   if (e != hipSuccess) {
     lt_ctx_destroy(c);
     return LT_ERR_HIP;
@@ -203,6 +227,7 @@ int lt_ctx_destroy(lt_ctx* c) {
   if (c->d_defer) (void)hipFree(c->d_defer);
   if (c->d_ndefer) (void)hipFree(c->d_ndefer);
   if (c->d_scene) (void)hipFree(c->d_scene);
+  if (c->d_xtab) (void)hipFree(c->d_xtab);
   if (c->h_scene) (void)hipHostFree(c->h_scene);
   delete c;
   return LT_OK;
@@ -319,7 +344,7 @@ int lt_analyze_tile(lt_ctx* c, const lt_scene* sc, const lt_params* prm, const l
   const bool few = prm->n_rules <= 4;
 #define LT_LAUNCH_FAST(MY, RM)                                                              \
   hipLaunchKernelGGL((analyze_fast_kernel<MY, RM>), fgrid, fblock, 0, stream, c->d_scene, *prm, \
-                     *in, *out, c->d_defer, c->d_ndefer)
+                     *in, *out, c->d_xtab, c->d_defer, c->d_ndefer)
   if (Y <= 32) {
     if (few) LT_LAUNCH_FAST(32, 4); else LT_LAUNCH_FAST(32, 16);
   } else if (Y <= 48) {
@@ -336,7 +361,7 @@ int lt_analyze_tile(lt_ctx* c, const lt_scene* sc, const lt_params* prm, const l
     const unsigned g = resolve_grid<MY, RM>(c->device);                                     \
     dim3 rg((unsigned)(nwave < (int64_t)g ? nwave : (int64_t)g));                           \
     hipLaunchKernelGGL((resolve_fast_kernel<MY, RM>), rg, fblock, 0, stream, c->d_scene,    \
-                       *prm, *in, *out, c->d_defer, c->d_ndefer);                           \
+                       *prm, *in, *out, c->d_xtab, c->d_defer, c->d_ndefer);                \
   } while (0)
   if (Y <= 32) {
     if (few) LT_LAUNCH_RESOLVE(32, 4); else LT_LAUNCH_RESOLVE(32, 16);

@@ -32,6 +32,26 @@ __device__ inline int wave_max(int v) {
   return __builtin_amdgcn_readfirstlane(v);
 }
 
+// Least squares of one segment per active lane, in lockstep: the x half (lsq_factor) comes from
+// the device x-set table when the lane's x values are there and is computed only for the lanes
+// that miss (a branch the wave takes only if some lane misses); then the y half for every lane.
+template <class GX, class GY>
+__device__ inline int lsq_lockstep(bool act, int m, GX X, GY Y, const lsq_xf* __restrict__ xtab,
+                                   bool need_solution, bool need_ssr, double& slope, double& icpt,
+                                   double& ssr) {
+  const int key = act ? xset_key(m, X) : 0;
+  const bool miss = act && key < 0;
+  lsq_xf f;
+  if (act && !miss) f = xtab[key];
+  if (__ballot(miss)) {
+    if (miss) lsq_factor(m, X, f);
+  }
+  slope = 0.0;
+  icpt = 0.0;
+  ssr = 0.0;
+  return act ? lsq_apply(f, X, Y, need_solution, need_ssr, slope, icpt, ssr) : 0;
+}
+
 // VT: storage type of the series. The analyze stage stores binary32 (pixels whose values are not
 // exact in binary32 are sent to the resolve stage), the resolve stage binary64.
 template <int MAXY, class VT>
@@ -48,8 +68,8 @@ struct WaveLds {
 // residual of each start inside the error window; always returns true.
 template <int MAXY, int RMAX, bool EXACT, class VT>
 __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const lt_tile_in& in,
-                                   const lt_tile_out& out, int64_t p, bool live, int lane,
-                                   WaveLds<MAXY, VT>& L) {
+                                   const lt_tile_out& out, const lsq_xf* __restrict__ xtab,
+                                   int64_t p, bool live, int lane, WaveLds<MAXY, VT>& L) {
   const int Y = S.n_years;
   const int64_t is = in.stride, os = out.stride;
   const double nan = __builtin_nan("");
@@ -248,10 +268,9 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
         double e = 0.0;
         if (__ballot(ls)) {
           double sm, sb, ssr;
-          const int rc = lstsq_xint(
-              ls ? m : 2, [&](int k) { return ls ? (int)L.xn[i + k][lane] : k; },
-              [&](int k) { return ls ? (double)L.ys[i + k][lane] : 0.0; }, false, true, sm, sb,
-              ssr);
+          const int rc = lsq_lockstep(
+              ls, m, [&](int k) { return (int)L.xn[i + k][lane]; },
+              [&](int k) { return (double)L.ys[i + k][lane]; }, xtab, false, true, sm, sb, ssr);
           if (ls) {
             if (rc < 0) status |= LT_ST_NUMERIC;
             e = ssr;
@@ -448,10 +467,9 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
     const int kbase = has_next ? ka : 0;
     double sm = 0.0, sbv = 0.0, ssr = 0.0;
     if (LT_ABLATE != 1 && __ballot(has_next)) {
-      const int rc = lstsq_xint(
-          mseg, [&](int k) { return has_next ? (int)L.xn[kbase + k][lane] : k; },
-          [&](int k) { return has_next ? (double)L.ys[kbase + k][lane] : 0.0; }, true, false,
-          sm, sbv, ssr);
+      const int rc = lsq_lockstep(
+          has_next, mseg, [&](int k) { return (int)L.xn[kbase + k][lane]; },
+          [&](int k) { return (double)L.ys[kbase + k][lane]; }, xtab, true, false, sm, sbv, ssr);
       if (has_next) {
         if (rc < 0) status |= LT_ST_NUMERIC;
         cm = sm;

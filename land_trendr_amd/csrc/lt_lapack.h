@@ -389,9 +389,19 @@ __host__ __device__ inline void dlasv2(double f, double g, double h, double& ssm
 }
 
 // DLALSD, N = 2: DLASDQ/DBDSQR on the 2x2 upper bidiagonal (d1, e; d2), solve, back-transform.
-// Returns the numerical rank, or -1 for the DLASCL rescaling path (not emulated).
-__host__ __device__ inline int dlalsd2(double d1, double d2, double e, double b1, double b2,
-                                       double rcond, double& x0, double& x1) {
+// Split in the part that depends on R = (d1, e; d2) only (dlalsd2_r: scaling, DLASV2 rotation,
+// sign fixes, the ascending re-sort, rank) and the part applied to b (dlalsd2_b), so a segment's
+// x-only factorisation can be computed once and reused (lsq_factor / lsq_apply below).
+struct lalsd2_r {
+  double mul, csl, snl, vt00, vt01, vt10, vt11, inv1, inv2;
+  int32_t rank;  // numerical rank 0..2, or -1 for the DLASCL rescaling path (not emulated)
+  uint8_t rot, swap, r1, r2;
+  uint8_t zero;  // org == 0: zero solution
+  uint8_t pad[3];
+};
+
+__host__ __device__ inline lalsd2_r dlalsd2_r(double d1, double d2, double e, double rcond) {
+  lalsd2_r R{};
   const double eps = 0x1p-53, unfl = 0x1p-1022;
   const double tolmul = 98.70149282610821;  // max(10, min(100, eps^(-1/8)))
   double rcnd = (rcond > 0.0 && rcond < 1.0) ? rcond : eps;
@@ -399,12 +409,15 @@ __host__ __device__ inline int dlalsd2(double d1, double d2, double e, double b1
   if (__builtin_fabs(d2) > org) org = __builtin_fabs(d2);
   if (__builtin_fabs(e) > org) org = __builtin_fabs(e);
   if (org == 0.0) {
-    x0 = 0.0;
-    x1 = 0.0;
-    return 0;
+    R.zero = 1;
+    R.rank = 0;
+    return R;
   }
-  if (!(org > 0x1p-900 && org < 0x1p900)) return -1;
-  double mul = 1.0 / org;
+  if (!(org > 0x1p-900 && org < 0x1p900)) {
+    R.rank = -1;
+    return R;
+  }
+  const double mul = 1.0 / org;
   d1 *= mul;
   d2 *= mul;
   e *= mul;
@@ -429,9 +442,9 @@ __host__ __device__ inline int dlalsd2(double d1, double d2, double e, double b1
     double a1 = vt01, c1 = vt11;
     vt01 = __builtin_fma(csr, a1, snr * c1);
     vt11 = __builtin_fma(csr, c1, -(snr * a1));
-    double p = b1, q = b2;
-    b1 = __builtin_fma(csl, p, snl * q);
-    b2 = __builtin_fma(csl, q, -(snl * p));
+    R.rot = 1;
+    R.csl = csl;
+    R.snl = snl;
   }
   if (d1 < 0.0) {
     d1 = -d1;
@@ -443,40 +456,66 @@ __host__ __device__ inline int dlalsd2(double d1, double d2, double e, double b1
     vt10 = -vt10;
     vt11 = -vt11;
   }
-  // DBDSQR leaves them descending; DLASDQ re-sorts ascending. Net: one swap iff d1 > d2 after
-  // the descending sort, i.e. swap when d1 != d2 ends up with the larger first.
-  if (d2 > d1) {
+  // DBDSQR leaves them descending, DLASDQ re-sorts ascending: net, one swap iff d1 > d2
+  if (d1 > d2) {
     double t = d1; d1 = d2; d2 = t;
     t = vt00; vt00 = vt10; vt10 = t;
     t = vt01; vt01 = vt11; vt11 = t;
-    t = b1; b1 = b2; b2 = t;
+    R.swap = 1;
   }
-  if (d2 < d1) {
-    double t = d1; d1 = d2; d2 = t;
-    t = vt00; vt00 = vt10; vt10 = t;
-    t = vt01; vt01 = vt11; vt11 = t;
-    t = b1; b1 = b2; b2 = t;
+  const double dmax = __builtin_fabs(d1) > __builtin_fabs(d2) ? __builtin_fabs(d1) : __builtin_fabs(d2);
+  const double tol2 = rcnd * dmax;
+  R.rank = 0;
+  if (!(d1 <= tol2)) {
+    R.inv1 = 1.0 / d1;
+    R.r1 = 1;
+    R.rank++;
   }
-  double dmax = __builtin_fabs(d1) > __builtin_fabs(d2) ? __builtin_fabs(d1) : __builtin_fabs(d2);
-  double tol2 = rcnd * dmax;
-  int rank = 0;
-  if (d1 <= tol2) {
-    b1 = 0.0;
-  } else {
-    b1 = b1 * (1.0 / d1);
-    rank++;
+  if (!(d2 <= tol2)) {
+    R.inv2 = 1.0 / d2;
+    R.r2 = 1;
+    R.rank++;
   }
-  if (d2 <= tol2) {
-    b2 = 0.0;
-  } else {
-    b2 = b2 * (1.0 / d2);
-    rank++;
+  R.mul = mul;
+  R.vt00 = vt00;
+  R.vt01 = vt01;
+  R.vt10 = vt10;
+  R.vt11 = vt11;
+  return R;
+}
+
+__host__ __device__ inline void dlalsd2_b(const lalsd2_r& R, double b1, double b2, double& x0,
+                                          double& x1) {
+  if (R.zero) {
+    x0 = 0.0;
+    x1 = 0.0;
+    return;
   }
-  double s0 = __builtin_fma(vt10, b2, vt00 * b1);
-  double s1 = __builtin_fma(vt11, b2, vt01 * b1);
-  x0 = s0 * mul;
-  x1 = s1 * mul;
-  return rank;
+  if (R.rot) {
+    const double p = b1, q = b2;
+    b1 = __builtin_fma(R.csl, p, R.snl * q);
+    b2 = __builtin_fma(R.csl, q, -(R.snl * p));
+  }
+  if (R.swap) {
+    const double t = b1;
+    b1 = b2;
+    b2 = t;
+  }
+  b1 = R.r1 ? b1 * R.inv1 : 0.0;
+  b2 = R.r2 ? b2 * R.inv2 : 0.0;
+  const double s0 = __builtin_fma(R.vt10, b2, R.vt00 * b1);
+  const double s1 = __builtin_fma(R.vt11, b2, R.vt01 * b1);
+  x0 = s0 * R.mul;
+  x1 = s1 * R.mul;
+}
+
+// Returns the numerical rank, or -1 for the DLASCL rescaling path (not emulated).
+__host__ __device__ inline int dlalsd2(double d1, double d2, double e, double b1, double b2,
+                                       double rcond, double& x0, double& x1) {
+  const lalsd2_r R = dlalsd2_r(d1, d2, e, rcond);
+  if (R.rank < 0) return -1;
+  dlalsd2_b(R, b1, b2, x0, x1);
+  return R.rank;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -606,12 +645,25 @@ __host__ __device__ inline f80 f80_from_u64(uint64_t s) {
   return f80{s << lz, 63 - lz};  // value = sig * 2^(exp - 63) = s
 }
 
-template <class GX, class GY>
-__host__ __device__ inline int lstsq_xint(int m, GX X, GY Y, bool need_solution, bool need_ssr,
-                                          double& slope, double& icpt, double& ssr) {
-  slope = 0.0;
-  icpt = 0.0;
-  ssr = 0.0;
+// The x-only half of lstsq_xint: everything that depends on the segment's x values alone (the
+// H1 reflector and the ones column it produces, H2 and its trimmed length, DLALSD's R part).
+// Segments with the same x values share it, so the analysis keeps a device table of the common
+// x-sets (lt_abi.hip) and applies only the y half per pixel. Identical operations in the same
+// order as one fused lstsq: lstsq_xint(m, X, Y) == lsq_apply(lsq_factor(m, X), X, Y) bit for bit.
+struct lsq_xf {
+  double s1, ntau1, sc;  // v1(k) = x_k * s1 (k >= 1); sb = ntau1 * (y . v1); C(k) = fma(sc, v1(k), 1)
+  double s2, ntau2;      // m >= 3: v2(k) = C(k+1) * s2 (k >= 1); sb2 = ntau2 * (b[1:] . v2)
+  lalsd2_r R;            // DLALSD on R = (beta1, r12; beta2)
+  int16_t m, lastv2;
+  int8_t rc;             // 0, or -4 (x not strictly increasing)
+  uint8_t tau2nz;
+  uint8_t pad[2];
+};
+
+template <class GX>
+__host__ __device__ inline void lsq_factor(int m, GX X, lsq_xf& f) {
+  f = lsq_xf{};
+  f.m = (int16_t)m;
   const double rcond = 0x1p-52 * (double)(m > 2 ? m : 2);
   // H1: alpha = x0, ||x[1:]|| from the exact integer sum of squares
   const int x0 = X(0);
@@ -619,7 +671,10 @@ __host__ __device__ inline int lstsq_xint(int m, GX X, GY Y, bool need_solution,
   int xprev = x0;
   for (int k = 1; k < m; k++) {
     const int xk = X(k);
-    if (xk <= xprev) return -4;
+    if (xk <= xprev) {
+      f.rc = -4;
+      return;
+    }
     xprev = xk;
     S += (uint64_t)((int64_t)xk * xk);
   }
@@ -633,69 +688,33 @@ __host__ __device__ inline int lstsq_xint(int m, GX X, GY Y, bool need_solution,
   const double beta1 = -__builtin_copysign(dlapy2(alpha, xn), alpha);  // xn > 0
   const double tau1 = (beta1 - alpha) / beta1;
   const double s1 = 1.0 / (alpha - beta1);
-  // pass A: gemv_t(ones, v1) and gemv_t(y, v1) (4 interleaved lanes + FMA tail), B == 0 test
+  // pass A, ones half: gemv_t(ones, v1) (4 interleaved lanes + FMA tail)
   const int m3 = m & 3, m1 = m - m3;
-  double A0 = 0.0, A1 = 0.0, A2 = 0.0, A3 = 0.0, Q0 = 0.0, Q1 = 0.0, Q2 = 0.0, Q3 = 0.0;
-  bool anyy = false;
-  double bmax = 0.0;
+  double A0 = 0.0, A1 = 0.0, A2 = 0.0, A3 = 0.0;
   for (int i = 0; i < m1; i += 4) {
-    const double v0 = i == 0 ? 1.0 : (double)X(i) * s1, va = (double)X(i + 1) * s1,
-                 vb = (double)X(i + 2) * s1, vc = (double)X(i + 3) * s1;
-    const double y0 = Y(i), ya = Y(i + 1), yb = Y(i + 2), yc = Y(i + 3);
-    A0 = A0 + v0;
-    A1 = A1 + va;
-    A2 = A2 + vb;
-    A3 = A3 + vc;
-    Q0 = Q0 + y0 * v0;
-    Q1 = Q1 + ya * va;
-    Q2 = Q2 + yb * vb;
-    Q3 = Q3 + yc * vc;
-    bmax = __builtin_fmax(bmax, __builtin_fmax(__builtin_fmax(__builtin_fabs(y0),
-                                                              __builtin_fabs(ya)),
-                                               __builtin_fmax(__builtin_fabs(yb),
-                                                              __builtin_fabs(yc))));
+    A0 = A0 + (i == 0 ? 1.0 : (double)X(i) * s1);
+    A1 = A1 + (double)X(i + 1) * s1;
+    A2 = A2 + (double)X(i + 2) * s1;
+    A3 = A3 + (double)X(i + 3) * s1;
   }
-  double wo = 0.0, wy = 0.0;
-  if (m1 > 0) {
-    wo = __builtin_fma((A0 + A2) + (A1 + A3), 1.0, 0.0);
-    wy = __builtin_fma((Q0 + Q2) + (Q1 + Q3), 1.0, 0.0);
-  }
+  double wo = 0.0;
+  if (m1 > 0) wo = __builtin_fma((A0 + A2) + (A1 + A3), 1.0, 0.0);
   auto v1 = [&](int k) { return k == 0 ? 1.0 : (double)X(k) * s1; };
-  if (m3 > 0) {
-    const double ta = v1(m1), ya = Y(m1);
-    bmax = __builtin_fmax(bmax, __builtin_fabs(ya));
-    if (m3 == 1) {
-      wo = __builtin_fma(1.0, ta, wo);
-      wy = __builtin_fma(ya, ta, wy);
-    } else {
-      const double tb = v1(m1 + 1), yb = Y(m1 + 1);
-      bmax = __builtin_fmax(bmax, __builtin_fabs(yb));
-      if (m3 == 2) {
-        wo = wo + __builtin_fma(1.0, ta, 1.0 * tb);
-        wy = wy + __builtin_fma(ya, ta, yb * tb);
-      } else {
-        const double tc = v1(m1 + 2), yc = Y(m1 + 2);
-        bmax = __builtin_fmax(bmax, __builtin_fabs(yc));
-        wo = wo + __builtin_fma(1.0, tc, __builtin_fma(1.0, ta, 1.0 * tb));
-        wy = wy + __builtin_fma(yc, tc, __builtin_fma(ya, ta, yb * tb));
-      }
-    }
+  if (m3 == 1) {
+    wo = __builtin_fma(1.0, v1(m1), wo);
+  } else if (m3 == 2) {
+    wo = wo + __builtin_fma(1.0, v1(m1), 1.0 * v1(m1 + 1));
+  } else if (m3 == 3) {
+    wo = wo + __builtin_fma(1.0, v1(m1 + 2), __builtin_fma(1.0, v1(m1), 1.0 * v1(m1 + 1)));
   }
-  anyy = bmax != 0.0;
-  if (!anyy) return 0;  // DGELSD: B == 0 -> zero solution, numpy reports no residual
-  if (!(bmax >= 0x1p-970 && bmax <= 0x1p970)) return -1;
   const double sc = (-tau1) * wo;
-  const double sb = (-tau1) * wy;  // DLARF applies the reflector: some y[k] != 0
   auto C = [&](int k) { return __builtin_fma(sc, v1(k), 1.0); };
-  auto B = [&](int k) { return __builtin_fma(sb, v1(k), Y(k)); };
+  f.s1 = s1;
+  f.ntau1 = -tau1;
+  f.sc = sc;
   if (m == 2) {
-    if (!need_solution) return 0;
-    double s0, sI;
-    const int rank = dlalsd2(beta1, C(1), C(0), B(0), B(1), rcond, s0, sI);
-    if (rank < 0) return -1;
-    slope = s0;
-    icpt = sI;
-    return rank == 2 ? 0 : -3;
+    f.R = dlalsd2_r(beta1, C(1), C(0), rcond);
+    return;
   }
   // pass B: H2 on c[1:], ||c[2:]|| in binary64 pairs (soft-float80 on the rare fallback)
   const double r12 = C(0), alpha2 = C(1);
@@ -708,13 +727,81 @@ __host__ __device__ inline int lstsq_xint(int m, GX X, GY Y, bool need_solution,
     tau2 = (beta2 - alpha2) / beta2;
     s2 = 1.0 / (alpha2 - beta2);
   }
-  auto v2 = [&](int k) { return k == 0 ? 1.0 : C(k + 1) * s2; };
-  // pass C: DLARF(v2, tau2) on b[1:]
   int lastv2 = m - 1;
+  if (tau2 != 0.0) {
+    auto v2 = [&](int k) { return k == 0 ? 1.0 : C(k + 1) * s2; };
+    while (lastv2 > 1 && v2(lastv2 - 1) == 0.0) lastv2--;
+  }
+  f.s2 = s2;
+  f.ntau2 = -tau2;
+  f.tau2nz = tau2 != 0.0;
+  f.lastv2 = (int16_t)lastv2;
+  f.R = dlalsd2_r(beta1, beta2, r12, rcond);
+}
+
+// The y half: DGELSD's B == 0 shortcut and range check, H1 and H2 applied to y, the residual
+// (need_ssr) and the solve (need_solution). X must give the x values f was factored from.
+template <class GX, class GY>
+__host__ __device__ inline int lsq_apply(const lsq_xf& f, GX X, GY Y, bool need_solution,
+                                         bool need_ssr, double& slope, double& icpt, double& ssr) {
+  slope = 0.0;
+  icpt = 0.0;
+  ssr = 0.0;
+  if (f.rc < 0) return f.rc;
+  const int m = f.m;
+  const double s1 = f.s1;
+  auto v1 = [&](int k) { return k == 0 ? 1.0 : (double)X(k) * s1; };
+  // pass A, y half: gemv_t(y, v1) (4 interleaved lanes + FMA tail), B == 0 test
+  const int m3 = m & 3, m1 = m - m3;
+  double Q0 = 0.0, Q1 = 0.0, Q2 = 0.0, Q3 = 0.0;
+  double bmax = 0.0;
+  for (int i = 0; i < m1; i += 4) {
+    const double y0 = Y(i), ya = Y(i + 1), yb = Y(i + 2), yc = Y(i + 3);
+    Q0 = Q0 + y0 * v1(i);
+    Q1 = Q1 + ya * v1(i + 1);
+    Q2 = Q2 + yb * v1(i + 2);
+    Q3 = Q3 + yc * v1(i + 3);
+    bmax = __builtin_fmax(bmax, __builtin_fmax(__builtin_fmax(__builtin_fabs(y0),
+                                                              __builtin_fabs(ya)),
+                                               __builtin_fmax(__builtin_fabs(yb),
+                                                              __builtin_fabs(yc))));
+  }
+  double wy = 0.0;
+  if (m1 > 0) wy = __builtin_fma((Q0 + Q2) + (Q1 + Q3), 1.0, 0.0);
+  if (m3 > 0) {
+    const double ta = v1(m1), ya = Y(m1);
+    bmax = __builtin_fmax(bmax, __builtin_fabs(ya));
+    if (m3 == 1) {
+      wy = __builtin_fma(ya, ta, wy);
+    } else {
+      const double tb = v1(m1 + 1), yb = Y(m1 + 1);
+      bmax = __builtin_fmax(bmax, __builtin_fabs(yb));
+      if (m3 == 2) {
+        wy = wy + __builtin_fma(ya, ta, yb * tb);
+      } else {
+        const double tc = v1(m1 + 2), yc = Y(m1 + 2);
+        bmax = __builtin_fmax(bmax, __builtin_fabs(yc));
+        wy = wy + __builtin_fma(yc, tc, __builtin_fma(ya, ta, yb * tb));
+      }
+    }
+  }
+  if (bmax == 0.0) return 0;  // DGELSD: B == 0 -> zero solution, numpy reports no residual
+  if (!(bmax >= 0x1p-970 && bmax <= 0x1p970)) return -1;
+  const double sb = f.ntau1 * wy;  // DLARF applies the reflector: some y[k] != 0
+  auto B = [&](int k) { return __builtin_fma(sb, v1(k), Y(k)); };
+  if (m == 2) {
+    if (!need_solution) return 0;
+    if (f.R.rank < 0) return -1;
+    dlalsd2_b(f.R, B(0), B(1), slope, icpt);
+    return f.R.rank == 2 ? 0 : -3;
+  }
+  const double sc = f.sc, s2 = f.s2;
+  auto v2 = [&](int k) { return k == 0 ? 1.0 : __builtin_fma(sc, v1(k + 1), 1.0) * s2; };
+  // pass C: DLARF(v2, tau2) on b[1:]
+  const int lastv2 = f.lastv2;
   double sb2 = 0.0;
   bool b2_upd = false;
-  if (tau2 != 0.0) {
-    while (lastv2 > 1 && v2(lastv2 - 1) == 0.0) lastv2--;
+  if (f.tau2nz) {
     bool any = false;
     const double w2 = gemv_t1(lastv2, [&](int k) {
       const double bk = B(k + 1);
@@ -722,7 +809,7 @@ __host__ __device__ inline int lstsq_xint(int m, GX X, GY Y, bool need_solution,
       return bk;
     }, v2);
     if (any) {
-      sb2 = (-tau2) * w2;
+      sb2 = f.ntau2 * w2;
       b2_upd = true;
     }
   }
@@ -738,14 +825,84 @@ __host__ __device__ inline int lstsq_xint(int m, GX X, GY Y, bool need_solution,
     }
   int rank = 2;
   if (need_solution) {
-    double s0, sI;
-    rank = dlalsd2(beta1, beta2, r12, B(0), B2(1), rcond, s0, sI);
-    if (rank < 0) return -1;
-    slope = s0;
-    icpt = sI;
+    if (f.R.rank < 0) return -1;
+    dlalsd2_b(f.R, B(0), B2(1), slope, icpt);
+    rank = f.R.rank;
   }
   ssr = rank == 2 ? res : 0.0;
   return rank == 2 ? 0 : -3;
+}
+
+template <class GX, class GY>
+__host__ __device__ inline int lstsq_xint(int m, GX X, GY Y, bool need_solution, bool need_ssr,
+                                          double& slope, double& icpt, double& ssr) {
+  lsq_xf f;
+  lsq_factor(m, X, f);
+  return lsq_apply(f, X, Y, need_solution, need_ssr, slope, icpt, ssr);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Table of lsq_factor results for the x-sets segments usually have (year offsets < 64): m = 2
+// with a gap <= 16, m = 3 with gaps <= 8, m = 4 with gaps <= 4, and m >= 5 consecutive years.
+// Built on the device once per context (lt_abi.hip); lookups that miss factor on the fly.
+// ------------------------------------------------------------------------------------------------
+constexpr int kXtM2 = 0, kXtM3 = 64 * 16, kXtM4 = kXtM3 + 64 * 64, kXtCons = kXtM4 + 64 * 64,
+              kXtSize = kXtCons + 64 * 64;
+
+// table slot of the x-set X(0) < ... < X(m-1) (all < 64), or -1
+template <class GX>
+__host__ __device__ inline int xset_key(int m, GX X) {
+  const int x0 = X(0);
+  if (x0 < 0 || x0 > 63) return -1;
+  if (m == 2) {
+    const int d = X(1) - x0;
+    return (d >= 1 && d <= 16) ? kXtM2 + x0 * 16 + (d - 1) : -1;
+  }
+  if (m == 3) {
+    const int x1 = X(1), d1 = x1 - x0, d2 = X(2) - x1;
+    return (d1 >= 1 && d1 <= 8 && d2 >= 1 && d2 <= 8) ? kXtM3 + x0 * 64 + (d1 - 1) * 8 + (d2 - 1)
+                                                      : -1;
+  }
+  if (m == 4) {
+    const int x1 = X(1), x2 = X(2), d1 = x1 - x0, d2 = x2 - x1, d3 = X(3) - x2;
+    return (d1 >= 1 && d1 <= 4 && d2 >= 1 && d2 <= 4 && d3 >= 1 && d3 <= 4)
+               ? kXtM4 + x0 * 64 + (d1 - 1) * 16 + (d2 - 1) * 4 + (d3 - 1)
+               : -1;
+  }
+  if (m >= 5 && m <= 64 && X(m - 1) - x0 == m - 1) return kXtCons + x0 * 64 + (m - 1);
+  return -1;
+}
+
+// the x-set of table slot idx: m and xs[0..m-1]; false for a slot no x-set maps to
+__host__ __device__ inline bool xset_of_key(int idx, int& m, int* xs) {
+  int d[3] = {1, 1, 1};
+  if (idx < kXtM3) {
+    m = 2;
+    xs[0] = idx / 16;
+    d[0] = idx % 16 + 1;
+  } else if (idx < kXtM4) {
+    const int r = idx - kXtM3;
+    m = 3;
+    xs[0] = r / 64;
+    d[0] = (r / 8) % 8 + 1;
+    d[1] = r % 8 + 1;
+  } else if (idx < kXtCons) {
+    const int r = idx - kXtM4;
+    m = 4;
+    xs[0] = r / 64;
+    d[0] = (r / 16) % 4 + 1;
+    d[1] = (r / 4) % 4 + 1;
+    d[2] = r % 4 + 1;
+  } else if (idx < kXtSize) {
+    const int r = idx - kXtCons;
+    m = r % 64 + 1;
+    xs[0] = r / 64;
+    if (m < 5) return false;
+  } else {
+    return false;
+  }
+  for (int k = 1; k < m; k++) xs[k] = xs[k - 1] + (m <= 4 ? d[k - 1] : 1);
+  return xs[m - 1] <= 63;
 }
 
 }  // namespace lt

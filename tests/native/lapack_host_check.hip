@@ -85,3 +85,16 @@ extern "C" int ltx_sqrt_pair(double hi, double lo, double* out2) {
   out2[1] = lt::f80_sqrt_to_double(lt::xdd_to_f80(lt::xdd{hi, lo}));
   return s;
 }
+
+// x-set table keys: round trip of every slot; returns the number of mismatches
+extern "C" int ltx_xset_roundtrip(int* n_valid) {
+  int bad = 0, nv = 0;
+  for (int idx = 0; idx < lt::kXtSize; idx++) {
+    int m = 0, xs[64];
+    if (!lt::xset_of_key(idx, m, xs)) continue;
+    nv++;
+    bad += lt::xset_key(m, [&](int k) { return xs[k]; }) != idx;
+  }
+  *n_valid = nv;
+  return bad;
+}

@@ -223,3 +223,11 @@ def test_pair_sqrt_matches_integer_f80(hc):
         bad += not golden_io._bits_equal(out[0], out[1])
     assert bad == 0
     assert nslow < N * 0.01
+
+
+def test_xset_table_keys_round_trip(hc):
+    """Every slot of the x-set factor table maps back to itself (lt_lapack.h xset_key)."""
+    nv = ctypes.c_int(0)
+    hc.ltx_xset_roundtrip.argtypes = [ctypes.POINTER(ctypes.c_int)]
+    assert hc.ltx_xset_roundtrip(ctypes.byref(nv)) == 0
+    assert nv.value > 8000
