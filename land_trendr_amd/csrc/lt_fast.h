@@ -244,11 +244,10 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
         if (m >= 3) w = __builtin_fma(0x1p-50, __builtin_fabs(v), kScreen * Syy);
         lo[i] = v - w;
         H = v + w < H ? v + w : H;
-        // early exit (same argument as the lazy DP): no start below i can reach H
+        // early exit (dp_start_bound): no start below i can reach H
         if (prune && m >= 3) {
           imin = i;
-          const double lb = (__builtin_fma(-2.0 * kScreen, SyyAll, e) + c) * (1.0 - 0x1p-50);
-          if (!__ballot(col && !(lb > H))) break;
+          if (!__ballot(col && !(dp_start_bound(e, OPT[i], 0.0, c, SyyAll) > H))) break;
         }
       }
       uint64_t cand = 0;  // starts whose interval reaches H: the exact minimum is among them
@@ -390,14 +389,11 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
         L2 = bl ? L1 : (lo < L2 ? lo : L2);
         L1 = bl ? lo : L1;
         iL = bl ? i : iL;
-        // early exit: a longer segment has a residual at least this one's (least squares on a
-        // superset of the points), OPT >= 0 (line_cost >= 0), so every start below i is worth
-        // at least lb: once lb exceeds the best upper end so far in every lane, none of them
-        // can be the minimum (or tie it), nor move a lower end that the decision reads
+        // early exit (dp_start_bound): once no start below i can reach the best upper end in
+        // any lane, the column is complete
         if (prune) {
-          const double lb = (__builtin_fma(-2.0 * kScreen, SyyAll, e) + c) * (1.0 - 0x1p-50);
           const double Hb = Hi < Ve ? Hi : Ve;
-          if (!__ballot(col && !(lb > Hb))) break;
+          if (!__ballot(col && !(dp_start_bound(e, OPTa[i], wopt, c, SyyAll) > Hb))) break;
         }
       }
       const double H = Hi < Ve ? Hi : Ve;  // the exact minimum lies in [min(L1, Ve), H]

@@ -162,6 +162,21 @@ struct RuleState {
 // (tests/test_screening.py), the closed form in double 2^-52: 2^-30 leaves a 2^18 margin.
 constexpr double kScreen = 0x1p-30;
 
+// Early exit over the starts of a DP column (the reference prices every start, utils.py:618-631;
+// starts are visited in decreasing order). For a start i' < i of column j, in exact arithmetic,
+//   e(i',j) >= e(i',i-1) + e(i,j)      (least squares on the union of two point sets)
+//   OPT[i]  <= OPT[i'] + e(i',i-1) + c (start i' is a candidate of OPT[i])
+// so v(i') = e(i',j) + c + OPT[i'] >= e(i,j) + OPT[i]; with c >= 0 (OPT >= 0) also >= e(i,j) + c.
+// The bound below holds for the reference's rounded values: eopt >= |opta - OPT_ref[i]|, each of
+// the three residuals involved is within kScreen * its sum(y^2) <= SyyAll of the exact one, and
+// the factors cover the roundings. Once it exceeds an upper bound on the column minimum, no start
+// below i can be (or tie) the minimum.
+__host__ __device__ inline double dp_start_bound(double e, double opta, double eopt, double c,
+                                                 double SyyAll) {
+  const double o = opta - eopt > c ? opta - eopt : c;
+  return (e + o) * (1.0 - 0x1p-49) - 4.0 * kScreen * SyyAll * (1.0 + 0x1p-49);
+}
+
 // segmented_least_squares' DP (utils.py:618-631) with candidate screening.
 // For column j every start i is first priced with the closed-form SSE of its segment (exact
 // integer sums for integer data); only the starts whose price lies within the error window of
@@ -205,10 +220,7 @@ __host__ __device__ inline void dp_screened(int n, const uint8_t* xs, const doub
       vmin = v < vmin ? v : vmin;
       wmax = w > wmax ? w : wmax;
       Hc = v + w < Hc ? v + w : Hc;
-      // early exit: a longer segment's residual is at least this one's (least squares on a
-      // superset), OPT >= 0 for line_cost >= 0, so every start below i is worth at least lb;
-      // lb > Hc >= the column minimum: none of them can be (or tie) the minimum
-      if (m >= 3 && c >= 0.0 && (e - 2.0 * kScreen * SyyAll + c) * (1.0 - 0x1p-50) > Hc) break;
+      if (m >= 3 && c >= 0.0 && dp_start_bound(e, OPT[i], 0.0, c, SyyAll) > Hc) break;
     }
     // pass 2: exact price for the starts inside the window, first exact minimum wins
     const double lim = vmin + 2.0 * wmax;
@@ -310,7 +322,7 @@ __host__ __device__ inline bool dp_lazy(int n, const uint8_t* xs, const double* 
         Li2 = lo;
       }
       const double Hc = Hi < Ve ? Hi : Ve;
-      if (m >= 3 && c >= 0.0 && (e - 2.0 * kScreen * SyyAll + c) * (1.0 - 0x1p-50) > Hc) break;
+      if (m >= 3 && c >= 0.0 && dp_start_bound(e, OPTa[i], E[i], c, SyyAll) > Hc) break;
     }
     const double H = Hi < Ve ? Hi : Ve;  // the exact minimum lies in [min lower bound, H]
     if (Li1 > H) {  // no interval reaches H: the exact candidates decide, bit-exactly
