@@ -82,41 +82,60 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
   int T = 0, y0 = 0;
   uint64_t pres = 0;  // year slots with a winner: present point t is the t-th set bit
   bool f32_bad = false;
-  for (int y = 0; y < Y; y++) {
-    int best = -1, bd = 0x7fffffff;
-    const int k1 = S.slot_begin[y + 1];
-    for (int k = S.slot_begin[y]; k < k1; k++) {
-      const int o = S.order[k];
-      const bool ok = live && (in.obs_valid == nullptr || in.obs_valid[(int64_t)o * is + p] != 0);
-      if (ok && S.dist[k] < bd) {
-        bd = S.dist[k];
-        best = o;
+  // years in batches of 8: the winners first, then their 8 value loads issued together (one
+  // load per year in sequence would leave each wave waiting out the HBM latency 30 times)
+  constexpr int WB = 8;
+  for (int yb = 0; yb < Y; yb += WB) {
+    int best[WB];
+#pragma unroll
+    for (int u = 0; u < WB; u++) {
+      const int y = yb + u;
+      best[u] = -1;
+      if (y >= Y) continue;  // wave-uniform
+      int bd = 0x7fffffff;
+      const int k1 = S.slot_begin[y + 1];
+      for (int k = S.slot_begin[y]; k < k1; k++) {
+        const int o = S.order[k];
+        const bool ok =
+            live && (in.obs_valid == nullptr || in.obs_valid[(int64_t)o * is + p] != 0);
+        if (ok && S.dist[k] < bd) {
+          bd = S.dist[k];
+          best[u] = o;
+        }
       }
     }
-    if (!live) continue;
-    const int64_t q = (int64_t)y * os + p;
-    if (out.winner) out.winner[q] = (int16_t)best;
-    if (best >= 0) {
-      if (S.feb29_bad[y]) status |= LT_ST_FEB29;
-      const double v = in.obs_val[(int64_t)best * is + p];
-      if (T == 0) y0 = S.year[y];
-      const VT vs = (VT)v;
-      if constexpr (!EXACT) {
-        if (!((double)vs == v)) f32_bad = true;
+    double val[WB];
+#pragma unroll
+    for (int u = 0; u < WB; u++)  // unconditional (obs 0 / pixel 0 stand in): all in flight
+      val[u] = in.obs_val[(int64_t)(best[u] >= 0 ? best[u] : 0) * is + (live ? p : 0)];
+#pragma unroll
+    for (int u = 0; u < WB; u++) {
+      const int y = yb + u;
+      if (y >= Y || !live) continue;
+      const int64_t q = (int64_t)y * os + p;
+      if (out.winner) out.winner[q] = (int16_t)best[u];
+      if (best[u] >= 0) {
+        if (S.feb29_bad[y]) status |= LT_ST_FEB29;
+        const double v = val[u];
+        if (T == 0) y0 = S.year[y];
+        const VT vs = (VT)v;
+        if constexpr (!EXACT) {
+          if (!((double)vs == v)) f32_bad = true;
+        }
+        L.ys[T][lane] = vs;
+        pres |= 1ull << y;
+        T++;
+        if (out.val_raw) out.val_raw[q] = v;
+      } else {
+        if (out.val_raw) out.val_raw[q] = nan;
+        if (out.val_fit) out.val_fit[q] = nan;
+        if (out.fit_m) out.fit_m[q] = nan;
+        if (out.fit_b) out.fit_b[q] = nan;
+        if (out.right_m) out.right_m[q] = nan;
+        if (out.right_b) out.right_b[q] = nan;
+        if (out.spike) out.spike[q] = 0;
+        if (out.vertex) out.vertex[q] = 0;
       }
-      L.ys[T][lane] = vs;
-      pres |= 1ull << y;
-      T++;
-      if (out.val_raw) out.val_raw[q] = v;
-    } else {
-      if (out.val_raw) out.val_raw[q] = nan;
-      if (out.val_fit) out.val_fit[q] = nan;
-      if (out.fit_m) out.fit_m[q] = nan;
-      if (out.fit_b) out.fit_b[q] = nan;
-      if (out.right_m) out.right_m[q] = nan;
-      if (out.right_b) out.right_b[q] = nan;
-      if (out.spike) out.spike[q] = 0;
-      if (out.vertex) out.vertex[q] = 0;
     }
   }
   // the reference raises for T < 2; non-binary32 values take the resolve stage's double path
