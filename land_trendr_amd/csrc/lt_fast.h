@@ -220,7 +220,6 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
     const double c = P.line_cost;
     const double inf = __builtin_inf();
     double OPT[MAXY + 1];
-    double lo[MAXY];
 #pragma unroll
     for (int k = 0; k <= MAXY; k++) OPT[k] = 0.0;
     double SyyAll = 0.0;  // sum of y^2 over the points 0..j (early-exit bound, as below)
@@ -231,7 +230,9 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
       double Sy = 0.0, Sxy = 0.0, Syy = 0.0;
       int Sx = 0, Sxx = 0;
       double H = inf;
-      int imin = 0;  // starts below imin were never priced (early exit)
+      // starts whose interval reaches the smallest upper end seen so far (itself included): a
+      // superset of those reaching the final one, where the exact minimum lies
+      uint64_t cand = 0;
       {
         const double yj = (double)L.ys[j][lane];
         SyyAll = __builtin_fma(yj, yj, SyyAll);
@@ -261,18 +262,12 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
         }
         const double v = (e + c) + OPT[i];
         if (m >= 3) w = __builtin_fma(0x1p-50, __builtin_fabs(v), kScreen * Syy);
-        lo[i] = v - w;
+        if (v - w <= H) cand |= 1ull << i;
         H = v + w < H ? v + w : H;
         // early exit (dp_start_bound): no start below i can reach H
-        if (prune && m >= 3) {
-          imin = i;
-          if (!__ballot(col && !(dp_start_bound(e, OPT[i], 0.0, c, SyyAll) > H))) break;
-        }
+        if (prune && m >= 3 && !__ballot(col && !(dp_start_bound(e, OPT[i], 0.0, c, SyyAll) > H)))
+          break;
       }
-      uint64_t cand = 0;  // starts whose interval reaches H: the exact minimum is among them
-#pragma unroll
-      for (int i = 0; i < MAXY; i++)
-        if (i <= j && i >= imin && lo[i] <= H) cand |= 1ull << i;
       const int nc = col ? __builtin_popcountll(cand) : 0;
       const int ncmax = wave_max(nc);
       double best = inf;
