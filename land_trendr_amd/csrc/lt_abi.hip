@@ -341,16 +341,16 @@ int lt_analyze_tile(lt_ctx* c, const lt_scene* sc, const lt_params* prm, const l
   const int64_t nwave = (in->n_pix + 63) / 64;
   if (nwave > 0x7fffffff) return fail(c, LT_ERR_LIMIT, "tile too large%s");
   dim3 fgrid((unsigned)nwave), fblock(64);
-  const bool few = prm->n_rules <= 4;
+  const bool one = prm->n_rules <= 1, few = prm->n_rules <= 4;
 #define LT_LAUNCH_FAST(MY, RM)                                                              \
   hipLaunchKernelGGL((analyze_fast_kernel<MY, RM>), fgrid, fblock, 0, stream, c->d_scene, *prm, \
                      *in, *out, c->d_xtab, c->d_defer, c->d_ndefer)
   if (Y <= 32) {
-    if (few) LT_LAUNCH_FAST(32, 4); else LT_LAUNCH_FAST(32, 16);
+    if (one) LT_LAUNCH_FAST(32, 1); else if (few) LT_LAUNCH_FAST(32, 4); else LT_LAUNCH_FAST(32, 16);
   } else if (Y <= 48) {
-    if (few) LT_LAUNCH_FAST(48, 4); else LT_LAUNCH_FAST(48, 16);
+    if (one) LT_LAUNCH_FAST(48, 1); else if (few) LT_LAUNCH_FAST(48, 4); else LT_LAUNCH_FAST(48, 16);
   } else {
-    if (few) LT_LAUNCH_FAST(64, 4); else LT_LAUNCH_FAST(64, 16);
+    if (one) LT_LAUNCH_FAST(64, 1); else if (few) LT_LAUNCH_FAST(64, 4); else LT_LAUNCH_FAST(64, 16);
   }
 #undef LT_LAUNCH_FAST
   HIP_OR_FAIL(c, hipGetLastError());
@@ -364,11 +364,11 @@ int lt_analyze_tile(lt_ctx* c, const lt_scene* sc, const lt_params* prm, const l
                        *prm, *in, *out, c->d_xtab, c->d_defer, c->d_ndefer);                \
   } while (0)
   if (Y <= 32) {
-    if (few) LT_LAUNCH_RESOLVE(32, 4); else LT_LAUNCH_RESOLVE(32, 16);
+    if (one) LT_LAUNCH_RESOLVE(32, 1); else if (few) LT_LAUNCH_RESOLVE(32, 4); else LT_LAUNCH_RESOLVE(32, 16);
   } else if (Y <= 48) {
-    if (few) LT_LAUNCH_RESOLVE(48, 4); else LT_LAUNCH_RESOLVE(48, 16);
+    if (one) LT_LAUNCH_RESOLVE(48, 1); else if (few) LT_LAUNCH_RESOLVE(48, 4); else LT_LAUNCH_RESOLVE(48, 16);
   } else {
-    if (few) LT_LAUNCH_RESOLVE(64, 4); else LT_LAUNCH_RESOLVE(64, 16);
+    if (one) LT_LAUNCH_RESOLVE(64, 1); else if (few) LT_LAUNCH_RESOLVE(64, 4); else LT_LAUNCH_RESOLVE(64, 16);
   }
 #undef LT_LAUNCH_RESOLVE
   HIP_OR_FAIL(c, hipGetLastError());
