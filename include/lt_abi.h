@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define LT_ABI_VERSION 1
+#define LT_ABI_VERSION 2
 #define LT_MAX_YEARS 64   /* distinct calendar years per scene (T <= 40 in every config) */
 #define LT_MAX_OBS 1024   /* observations per scene (K*T) */
 #define LT_MAX_RULES 16
@@ -92,12 +92,58 @@ typedef struct {
   const uint8_t* feb29_bad;   /* [Y]   1: target is Feb-29 and year y is not a leap year     */
 } lt_scene;
 
+/* Element types of raster planes (the GDAL band types a LandTrendr stack meets). */
+enum { LT_T_F64 = 0, LT_T_I16 = 1, LT_T_U16 = 2, LT_T_I32 = 3, LT_T_F32 = 4, LT_T_U8 = 5,
+       LT_T_U32 = 6, LT_T_I8 = 7, LT_T_I64 = 8 };
 typedef struct {
   int64_t n_pix;              /* P                                                          */
   int64_t stride;             /* elements between obs planes (>= n_pix)                     */
   const double* obs_val;      /* [K][stride] observation values (float(val), utils.py:357)  */
   const uint8_t* obs_valid;   /* [K][stride] 0 = cloud-masked (utils.py:353); NULL = all    */
+  const void* obs_index;      /* [K][stride] the index raster in its stored type (typically */
+                              /* what lt_index_apply wrote); used instead of obs_val if set */
+  int32_t index_type;         /* LT_T_* of obs_index                                       */
+  int32_t _pad;
 } lt_tile_in;
+
+/* ---- load stage: settings.json index_eqn (utils.py:447-484 rast_algebra) -------------------- */
+#define LT_MAX_PROG 64
+#define LT_MAX_BANDS 16
+enum { LT_OP_BAND = 1,      /* push band plane ival (0-based slot), in band_type               */
+       LT_OP_CONST_I = 2,   /* push the integer ival                                            */
+       LT_OP_CONST_F = 3,   /* push the double fval                                             */
+       LT_OP_ADD = 4, LT_OP_SUB = 5, LT_OP_MUL = 6,
+       LT_OP_DIV = 7,       /* Python 2 '/': floor division on integer types, true on floats    */
+       LT_OP_FLOORDIV = 8,  /* '//'                                                             */
+       LT_OP_NEG = 9 };
+/* One postfix operation. `type` is the numpy result type of the node (binary ops: both operands
+ * are cast to it first, as numpy does); integer results wrap. */
+typedef struct {
+  int32_t op;
+  int32_t type;               /* LT_T_*                                                     */
+  int64_t ival;
+  double fval;
+} lt_index_op;
+/* A typed program built and validated by the host (land_trendr_amd/index_eqn.py). */
+typedef struct {
+  int32_t n_ops;
+  int32_t n_bands;            /* band planes per observation                                */
+  int32_t band_type;          /* LT_T_* of every band plane                                 */
+  int32_t out_type;           /* LT_T_* the index raster is stored in (the template's type) */
+  lt_index_op ops[LT_MAX_PROG];
+} lt_index_prog;
+/* Device buffers of one lt_index_apply: band s of obs o, pixel p at
+ * bands[o*obs_stride + s*band_stride + p]; index of obs o, pixel p at out[o*out_stride + p]. */
+typedef struct {
+  int64_t n_pix;
+  int64_t n_obs;
+  int64_t obs_stride;
+  int64_t band_stride;
+  int64_t out_stride;
+  const void* bands;
+  void* out;
+} lt_index_io;
+typedef struct lt_index lt_index;
 
 typedef struct {
   int64_t stride;             /* elements between year / rule planes (>= n_pix)             */
@@ -160,6 +206,15 @@ int lt_ctx_set_timing(lt_ctx* ctx, int enable);
 int lt_ctx_stage_ms(lt_ctx* ctx, double* ms_out, int n_stages, int64_t* n_launches);
 /* Pixels the last lt_analyze_tile deferred to the resolve stage (synchronous read). */
 int lt_ctx_last_deferred(lt_ctx* ctx, int64_t* n_deferred);
+
+/* Load stage. lt_index_codegen writes the HIP source generated for `prog` (for inspection and the
+ * CPU tests; returns the length, or a negative LT_ERR_*). lt_index_compile builds it with hiprtc
+ * for the context's device (cached per program inside the context; LT_ERR_JIT with the compiler
+ * log in lt_last_error on failure). lt_index_apply computes the index raster of every observation
+ * of a tile — rast_algebra's eval, then the store into out_type — asynchronously on `stream`. */
+int lt_index_codegen(const lt_index_prog* prog, char* buf, int64_t cap);
+int lt_index_compile(lt_ctx* ctx, const lt_index_prog* prog, lt_index** out);
+int lt_index_apply(lt_ctx* ctx, const lt_index* fn, const lt_index_io* io, void* stream);
 
 #ifdef __cplusplus
 }

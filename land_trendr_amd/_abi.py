@@ -10,7 +10,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, 'liblt_hip.so')
 
-LT_ABI_VERSION = 1
+LT_ABI_VERSION = 2
 LT_MAX_YEARS = 64
 LT_MAX_OBS = 1024
 LT_MAX_RULES = 16
@@ -27,6 +27,14 @@ c_i32p = ctypes.POINTER(ctypes.c_int32)
 c_i16p = ctypes.POINTER(ctypes.c_int16)
 c_u8p = ctypes.POINTER(ctypes.c_uint8)
 c_f64p = ctypes.POINTER(ctypes.c_double)
+
+# raster element types and the load-stage program (index_eqn)
+(LT_T_F64, LT_T_I16, LT_T_U16, LT_T_I32, LT_T_F32, LT_T_U8, LT_T_U32, LT_T_I8,
+ LT_T_I64) = range(9)
+LT_MAX_PROG = 64
+LT_MAX_BANDS = 16
+(LT_OP_BAND, LT_OP_CONST_I, LT_OP_CONST_F, LT_OP_ADD, LT_OP_SUB, LT_OP_MUL, LT_OP_DIV,
+ LT_OP_FLOORDIV, LT_OP_NEG) = range(1, 10)
 
 
 class LtRule(ctypes.Structure):
@@ -50,7 +58,26 @@ class LtScene(ctypes.Structure):
 
 class LtTileIn(ctypes.Structure):
     _fields_ = [('n_pix', ctypes.c_int64), ('stride', ctypes.c_int64), ('obs_val', c_f64p),
-                ('obs_valid', c_u8p)]
+                ('obs_valid', c_u8p), ('obs_index', ctypes.c_void_p),
+                ('index_type', ctypes.c_int32), ('_pad', ctypes.c_int32)]
+
+
+class LtIndexOp(ctypes.Structure):
+    _fields_ = [('op', ctypes.c_int32), ('type', ctypes.c_int32), ('ival', ctypes.c_int64),
+                ('fval', ctypes.c_double)]
+
+
+class LtIndexProg(ctypes.Structure):
+    _fields_ = [('n_ops', ctypes.c_int32), ('n_bands', ctypes.c_int32),
+                ('band_type', ctypes.c_int32), ('out_type', ctypes.c_int32),
+                ('ops', LtIndexOp * LT_MAX_PROG)]
+
+
+class LtIndexIO(ctypes.Structure):
+    _fields_ = [('n_pix', ctypes.c_int64), ('n_obs', ctypes.c_int64),
+                ('obs_stride', ctypes.c_int64), ('band_stride', ctypes.c_int64),
+                ('out_stride', ctypes.c_int64), ('bands', ctypes.c_void_p),
+                ('out', ctypes.c_void_p)]
 
 
 class LtTileOut(ctypes.Structure):
@@ -79,7 +106,7 @@ PIX_FIELDS = [('status', 'int32'), ('n_years', 'int32')]
 # symbols include/lt_abi.h declares (checked by tests/test_abi.py)
 EXPORTS = ['lt_abi_version', 'lt_ctx_create', 'lt_ctx_destroy', 'lt_last_error',
            'lt_analyze_tile', 'lt_label_tile', 'lt_ctx_set_timing', 'lt_ctx_stage_ms',
-           'lt_ctx_last_deferred']
+           'lt_ctx_last_deferred', 'lt_index_codegen', 'lt_index_compile', 'lt_index_apply']
 
 _LIB = None
 
@@ -108,6 +135,11 @@ def load_lib(path=None):
     lib.lt_ctx_set_timing.argtypes = [vp, ctypes.c_int]
     lib.lt_ctx_stage_ms.argtypes = [vp, c_f64p, ctypes.c_int, ctypes.POINTER(ctypes.c_int64)]
     lib.lt_ctx_last_deferred.argtypes = [vp, ctypes.POINTER(ctypes.c_int64)]
+    lib.lt_index_codegen.argtypes = [ctypes.POINTER(LtIndexProg), ctypes.c_char_p,
+                                     ctypes.c_int64]
+    lib.lt_index_codegen.restype = ctypes.c_int
+    lib.lt_index_compile.argtypes = [vp, ctypes.POINTER(LtIndexProg), ctypes.POINTER(vp)]
+    lib.lt_index_apply.argtypes = [vp, vp, ctypes.POINTER(LtIndexIO), vp]
     if lib.lt_abi_version() != LT_ABI_VERSION:
         raise RuntimeError('liblt_hip.so ABI %d != %d' % (lib.lt_abi_version(), LT_ABI_VERSION))
     if path is None:

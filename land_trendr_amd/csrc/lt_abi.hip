@@ -7,12 +7,14 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <map>
 #include <string>
 #include <vector>
 
 #include "../../include/lt_abi.h"
 #include "lt_fast.h"
 #include "lt_pixel.h"
+#include "lt_index.h"
 
 namespace {
 
@@ -167,6 +169,7 @@ struct lt_ctx {
   unsigned long long* d_ndefer = nullptr;
   int64_t defer_cap = 0;
   lt::lsq_xf* d_xtab = nullptr;  // x-set factor table (built at context creation)
+  std::map<std::string, lt_index*> index_fns;  // compiled load-stage kernels, by source
 };
 
 static int fail(lt_ctx* c, int code, const char* fmt, const char* detail = "") {
@@ -228,6 +231,10 @@ int lt_ctx_destroy(lt_ctx* c) {
   if (c->d_ndefer) (void)hipFree(c->d_ndefer);
   if (c->d_scene) (void)hipFree(c->d_scene);
   if (c->d_xtab) (void)hipFree(c->d_xtab);
+  for (auto& kv : c->index_fns) {
+    if (kv.second->mod) (void)hipModuleUnload(kv.second->mod);
+    delete kv.second;
+  }
   if (c->h_scene) (void)hipHostFree(c->h_scene);
   delete c;
   return LT_OK;
@@ -265,7 +272,9 @@ int lt_analyze_tile(lt_ctx* c, const lt_scene* sc, const lt_params* prm, const l
   if (in->n_pix < 0 || in->stride < in->n_pix || out->stride < in->n_pix)
     return fail(c, LT_ERR_ARG, "bad n_pix/stride%s");
   if (in->n_pix == 0) return LT_OK;
-  if (!in->obs_val) return fail(c, LT_ERR_ARG, "obs_val is required%s");
+  if (!in->obs_val && !in->obs_index) return fail(c, LT_ERR_ARG, "obs_val or obs_index required%s");
+  if (in->obs_index && !lt_idx::ctype(in->index_type))
+    return fail(c, LT_ERR_ARG, "bad index_type%s");
   const int K = sc->n_obs, Y = sc->n_years;
   if (K < 0 || K > LT_MAX_OBS || Y < 0 || Y > LT_MAX_YEARS)
     return fail(c, LT_ERR_LIMIT, "scene exceeds LT_MAX_OBS/LT_MAX_YEARS%s");
@@ -413,3 +422,88 @@ int lt_label_tile(lt_ctx* c, const lt_label_in* in, const lt_params* prm, const 
 }
 
 }  // extern "C"
+
+// ---- load stage (lt_index.h) ------------------------------------------------------------------
+int lt_index_codegen(const lt_index_prog* prog, char* buf, int64_t cap) {
+  if (!prog) return LT_ERR_ARG;
+  std::string err;
+  const std::string src = lt_idx::codegen(*prog, err);
+  if (src.empty()) return LT_ERR_ARG;
+  if (buf && cap > 0) {
+    const size_t n = src.size() < (size_t)(cap - 1) ? src.size() : (size_t)(cap - 1);
+    memcpy(buf, src.data(), n);
+    buf[n] = 0;
+  }
+  return (int)src.size();
+}
+
+int lt_index_compile(lt_ctx* c, const lt_index_prog* prog, lt_index** out) {
+  if (!c) return LT_ERR_ARG;
+  if (!prog || !out) return fail(c, LT_ERR_ARG, "null argument%s");
+  *out = nullptr;
+  std::string err;
+  const std::string src = lt_idx::codegen(*prog, err);
+  if (src.empty()) return fail(c, LT_ERR_ARG, "%s", err.c_str());
+  auto it = c->index_fns.find(src);
+  if (it != c->index_fns.end()) {
+    *out = it->second;
+    return LT_OK;
+  }
+  HIP_OR_FAIL(c, hipSetDevice(c->device));
+  hipDeviceProp_t prop;
+  HIP_OR_FAIL(c, hipGetDeviceProperties(&prop, c->device));
+  const std::string arch = std::string("--offload-arch=") + prop.gcnArchName;
+  hiprtcProgram rp;
+  if (hiprtcCreateProgram(&rp, src.c_str(), "lt_index.hip", 0, nullptr, nullptr) !=
+      HIPRTC_SUCCESS)
+    return fail(c, LT_ERR_JIT, "hiprtcCreateProgram failed%s");
+  const char* opts[] = {arch.c_str(), "-O3", "-ffp-contract=off"};
+  const hiprtcResult rc = hiprtcCompileProgram(rp, 3, opts);
+  if (rc != HIPRTC_SUCCESS) {
+    size_t n = 0;
+    hiprtcGetProgramLogSize(rp, &n);
+    std::string log(n, '\0');
+    if (n) hiprtcGetProgramLog(rp, &log[0]);
+    hiprtcDestroyProgram(&rp);
+    return fail(c, LT_ERR_JIT, "hiprtc: %s", log.c_str());
+  }
+  size_t code_size = 0;
+  hiprtcGetCodeSize(rp, &code_size);
+  std::vector<char> code(code_size);
+  hiprtcGetCode(rp, code.data());
+  hiprtcDestroyProgram(&rp);
+  lt_index* f = new lt_index();
+  f->n_bands = prog->n_bands;
+  f->band_type = prog->band_type;
+  f->out_type = prog->out_type;
+  if (hipModuleLoadData(&f->mod, code.data()) != hipSuccess ||
+      hipModuleGetFunction(&f->fn, f->mod, "lt_index_kernel") != hipSuccess) {
+    if (f->mod) (void)hipModuleUnload(f->mod);
+    delete f;
+    return fail(c, LT_ERR_JIT, "module load failed%s");
+  }
+  c->index_fns[src] = f;
+  *out = f;
+  return LT_OK;
+}
+
+int lt_index_apply(lt_ctx* c, const lt_index* f, const lt_index_io* io, void* stream_) {
+  if (!c) return LT_ERR_ARG;
+  if (!f || !io) return fail(c, LT_ERR_ARG, "null argument%s");
+  if (io->n_pix < 0 || io->n_obs < 0 || io->n_obs > 65535) return fail(c, LT_ERR_ARG, "bad sizes%s");
+  if (io->n_pix == 0 || io->n_obs == 0) return LT_OK;
+  if (!io->bands || !io->out) return fail(c, LT_ERR_ARG, "null buffer%s");
+  if (io->out_stride < io->n_pix || io->band_stride < io->n_pix ||
+      io->obs_stride < (int64_t)f->n_bands * io->band_stride)
+    return fail(c, LT_ERR_ARG, "bad strides%s");
+  HIP_OR_FAIL(c, hipSetDevice(c->device));
+  const void* bands = io->bands;
+  void* outp = io->out;
+  long long obs_stride = io->obs_stride, band_stride = io->band_stride, n_pix = io->n_pix,
+            out_stride = io->out_stride;
+  void* args[] = {(void*)&bands, &obs_stride, &band_stride, &n_pix, &outp, &out_stride};
+  const unsigned gx = (unsigned)((io->n_pix + 255) / 256);
+  HIP_OR_FAIL(c, hipModuleLaunchKernel(f->fn, gx, (unsigned)io->n_obs, 1, 256, 1, 1, 0,
+                                       (hipStream_t)stream_, args, nullptr));
+  return LT_OK;
+}

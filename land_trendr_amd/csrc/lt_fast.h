@@ -107,7 +107,7 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
     double val[WB];
 #pragma unroll
     for (int u = 0; u < WB; u++)  // unconditional (obs 0 / pixel 0 stand in): all in flight
-      val[u] = in.obs_val[(int64_t)(best[u] >= 0 ? best[u] : 0) * is + (live ? p : 0)];
+      val[u] = obs_value(in, (int64_t)(best[u] >= 0 ? best[u] : 0) * is + (live ? p : 0));
 #pragma unroll
     for (int u = 0; u < WB; u++) {
       const int y = yb + u;

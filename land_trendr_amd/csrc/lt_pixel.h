@@ -162,6 +162,23 @@ struct RuleState {
 // (tests/test_screening.py), the closed form in double 2^-52: 2^-30 leaves a 2^18 margin.
 constexpr double kScreen = 0x1p-30;
 
+// Observation value i of a tile: the f64 values, or the index raster in its stored type
+// (float(val), utils.py:357). index_type is uniform over a launch: a scalar branch on the GPU.
+__host__ __device__ inline double obs_value(const lt_tile_in& in, int64_t i) {
+  if (in.obs_index == nullptr) return in.obs_val[i];
+  switch (in.index_type) {
+    case LT_T_I16: return (double)((const int16_t*)in.obs_index)[i];
+    case LT_T_U16: return (double)((const uint16_t*)in.obs_index)[i];
+    case LT_T_I32: return (double)((const int32_t*)in.obs_index)[i];
+    case LT_T_F32: return (double)((const float*)in.obs_index)[i];
+    case LT_T_U8: return (double)((const uint8_t*)in.obs_index)[i];
+    case LT_T_U32: return (double)((const uint32_t*)in.obs_index)[i];
+    case LT_T_I8: return (double)((const int8_t*)in.obs_index)[i];
+    case LT_T_I64: return (double)((const int64_t*)in.obs_index)[i];
+    default: return ((const double*)in.obs_index)[i];
+  }
+}
+
 // Early exit over the starts of a DP column (the reference prices every start, utils.py:618-631;
 // starts are visited in decreasing order). For a start i' < i of column j, in exact arithmetic,
 //   e(i',j) >= e(i',i-1) + e(i,j)      (least squares on the union of two point sets)
@@ -373,7 +390,7 @@ __host__ __device__ bool analyze_pixel(const DevScene& S, const lt_params& P, co
     if (out.winner) out.winner[(int64_t)y * os + p] = (int16_t)best;
     if (best >= 0) {
       if (S.feb29_bad[y]) status |= LT_ST_FEB29;
-      val[T] = in.obs_val[(int64_t)best * is + p];
+      val[T] = obs_value(in, (int64_t)best * is + p);
       slot[T] = (uint8_t)y;
       T++;
     }

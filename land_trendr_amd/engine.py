@@ -16,6 +16,11 @@ LABEL_FIELDS = ('status', 'matched', 'class_val', 'onset_year', 'duration', 'mag
 
 _DT = {'int16': torch.int16, 'int32': torch.int32, 'uint8': torch.uint8,
        'float64': torch.float64}
+# raster element types a tile may carry (index rasters, band planes): torch dtype -> LT_T_*
+_LT_T = {torch.float64: _abi.LT_T_F64, torch.int16: _abi.LT_T_I16, torch.uint16: _abi.LT_T_U16,
+         torch.int32: _abi.LT_T_I32, torch.float32: _abi.LT_T_F32, torch.uint8: _abi.LT_T_U8,
+         torch.uint32: _abi.LT_T_U32, torch.int8: _abi.LT_T_I8, torch.int64: _abi.LT_T_I64}
+_TORCH_OF_LT = {v: k for k, v in _LT_T.items()}
 _SHAPE_KIND = {**{f: 'year' for f, _ in _abi.YEAR_FIELDS},
                **{f: 'rule' for f, _ in _abi.RULE_FIELDS},
                **{f: 'pix' for f, _ in _abi.PIX_FIELDS}}
@@ -67,10 +72,12 @@ class Engine:
 
     def analyze_tile(self, scene, params, values, valid=None, fields=ALL_FIELDS, out=None,
                      stream=None):
-        """values: float64 [K, P] (or a [K, stride] view's base), valid: uint8 [K, P] or None.
-        Returns the dict of output tensors ([Y, P], [R, P], [P]); asynchronous on `stream`."""
-        if values.dtype != torch.float64 or values.device != self.device or values.dim() != 2:
-            raise LtError('values must be a float64 [K, P] tensor on %s' % self.device)
+        """values: [K, P] observation values — float64, or an index raster in its stored type
+        (int16, uint16, int32, float32, uint8, ...: what index_tile writes) — valid: uint8 [K, P]
+        or None. Returns the dict of output tensors ([Y, P], [R, P], [P]); asynchronous on
+        `stream`."""
+        if values.dtype not in _LT_T or values.device != self.device or values.dim() != 2:
+            raise LtError('values must be a [K, P] raster tensor on %s' % self.device)
         if values.stride(1) != 1:
             raise LtError('values must have unit pixel stride')
         K, P = values.shape
@@ -99,7 +106,11 @@ class Engine:
         tin = _abi.LtTileIn()
         tin.n_pix = P
         tin.stride = values.stride(0)
-        tin.obs_val = ctypes.cast(values.data_ptr(), _abi.c_f64p)
+        if values.dtype == torch.float64:
+            tin.obs_val = ctypes.cast(values.data_ptr(), _abi.c_f64p)
+        else:
+            tin.obs_index = values.data_ptr()
+            tin.index_type = _LT_T[values.dtype]
         tin.obs_valid = ctypes.cast(valid.data_ptr(), _abi.c_u8p) if valid is not None else None
         tout = _abi.LtTileOut()
         tout.stride = ostride if ostride is not None else P
@@ -111,6 +122,42 @@ class Engine:
                                       ctypes.byref(tin), ctypes.byref(tout),
                                       ctypes.c_void_p(st.cuda_stream))
         self._check(rc, 'lt_analyze_tile')
+        return out
+
+    # --- load stage: index_eqn (rast_algebra, utils.py:447-484) ---
+    def compile_index(self, program):
+        """hiprtc-compile an index_eqn.IndexProgram for this device (cached per program)."""
+        fn = ctypes.c_void_p()
+        prog = program.to_c()
+        with torch.cuda.device(self.device):
+            self._check(self.lib.lt_index_compile(self.ctx, ctypes.byref(prog), ctypes.byref(fn)),
+                        'lt_index_compile')
+        return IndexFn(fn, program)
+
+    def index_tile(self, fn, bands, out=None, stream=None):
+        """bands: [K, NB, P] band planes (NB = the program's band slots, unit pixel stride) in
+        the program's band type; returns the [K, P] index raster in the program's output type."""
+        prog = fn.program
+        want = _TORCH_OF_LT[_LT_T_OF_NP(prog.band_dtype)]
+        if bands.dim() != 3 or bands.dtype != want or bands.device != self.device:
+            raise LtError('bands must be a %s [K, %d, P] tensor on %s' % (want, len(prog.bands),
+                                                                         self.device))
+        K, NB, P = bands.shape
+        if NB != len(prog.bands) or bands.stride(2) != 1:
+            raise LtError('bands must have %d band planes and unit pixel stride' % len(prog.bands))
+        odt = _TORCH_OF_LT[_LT_T_OF_NP(prog.out_dtype)]
+        if out is None:
+            out = torch.empty((K, P), dtype=odt, device=self.device)
+        if out.dtype != odt or out.shape[0] < K or out.shape[1] < P or out.stride(1) != 1:
+            raise LtError('out must be a %s [K, P] tensor' % odt)
+        io = _abi.LtIndexIO()
+        io.n_pix, io.n_obs = P, K
+        io.obs_stride, io.band_stride = bands.stride(0), bands.stride(1)
+        io.out_stride = out.stride(0)
+        io.bands, io.out = bands.data_ptr(), out.data_ptr()
+        st = stream if stream is not None else torch.cuda.current_stream(self.device)
+        self._check(self.lib.lt_index_apply(self.ctx, fn.handle, ctypes.byref(io),
+                                            ctypes.c_void_p(st.cuda_stream)), 'lt_index_apply')
         return out
 
     # --- stage timing (HIP events recorded around every launch on the launch stream) ---
@@ -127,6 +174,19 @@ class Engine:
         n = ctypes.c_int64()
         self._check(self.lib.lt_ctx_last_deferred(self.ctx, ctypes.byref(n)), 'last_deferred')
         return n.value
+
+
+class IndexFn:
+    """A compiled load-stage kernel (owned by the engine's context)."""
+
+    def __init__(self, handle, program):
+        self.handle = handle
+        self.program = program
+
+
+def _LT_T_OF_NP(np_dtype):
+    from .index_eqn import DTYPES
+    return DTYPES[np_dtype]
 
 
 _ENGINES = {}

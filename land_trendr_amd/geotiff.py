@@ -1,0 +1,119 @@
+"""Minimal GeoTIFF reader for co-registered Landsat stacks (SURVEY.md §8(f)-2 ingest, first piece).
+
+The reference reads rasters with GDAL (`ds2array`, utils.py:272-282; `rast_algebra` :447-484);
+GDAL is not in this image. This reads the baseline TIFF subset such stacks use: little- or
+big-endian classic TIFF, strips or tiles, no compression (Compression = 1), chunky or planar
+bands, sample formats uint/int/float of 8/16/32/64 bits, plus the GeoTIFF/GDAL tags kept as raw
+values (ModelPixelScale, ModelTiepoint, GeoKeyDirectory, GDAL_NODATA). Returns numpy arrays in
+the file's sample type, [bands, rows, cols] — what `ds2array(ds, b)` gives per band.
+"""
+import struct
+
+import numpy as np
+
+_TYPES = {1: ('B', 1), 2: ('s', 1), 3: ('H', 2), 4: ('I', 4), 5: ('II', 8), 6: ('b', 1),
+          7: ('B', 1), 8: ('h', 2), 9: ('i', 4), 10: ('ii', 8), 11: ('f', 4), 12: ('d', 8),
+          16: ('Q', 8), 17: ('q', 8)}
+_SAMPLE = {(1, 8): np.uint8, (1, 16): np.uint16, (1, 32): np.uint32, (1, 64): np.uint64,
+           (2, 8): np.int8, (2, 16): np.int16, (2, 32): np.int32, (2, 64): np.int64,
+           (3, 32): np.float32, (3, 64): np.float64}
+
+
+class TiffError(ValueError):
+    pass
+
+
+class GeoTiff:
+    def __init__(self, path):
+        with open(path, 'rb') as f:
+            self._d = f.read()
+        d = self._d
+        if d[:2] == b'II':
+            self._bo = '<'
+        elif d[:2] == b'MM':
+            self._bo = '>'
+        else:
+            raise TiffError('%s: not a TIFF file' % path)
+        magic, off = struct.unpack(self._bo + 'HI', d[2:8])
+        if magic != 42:
+            raise TiffError('%s: BigTIFF / unknown TIFF version %d' % (path, magic))
+        self.tags = self._ifd(off)
+        t = self.tags
+        self.width = int(t[256][0])
+        self.height = int(t[257][0])
+        bps = t.get(258, (1,))
+        self.bits = int(bps[0])
+        if any(int(b) != self.bits for b in bps):
+            raise TiffError('mixed bits per sample')
+        self.bands = int(t.get(277, (1,))[0])
+        fmt = int(t.get(339, (1,))[0])
+        if int(t.get(259, (1,))[0]) != 1:
+            raise TiffError('compressed TIFF (Compression=%d) is not supported' % t[259][0])
+        if (fmt, self.bits) not in _SAMPLE:
+            raise TiffError('sample format %d / %d bits not supported' % (fmt, self.bits))
+        self.dtype = np.dtype(_SAMPLE[(fmt, self.bits)]).newbyteorder(self._bo)
+        self.planar = int(t.get(284, (1,))[0])
+        nd = t.get(42113)
+        self.nodata = float(nd.rstrip('\x00')) if nd else None
+        self.pixel_scale = t.get(33550)
+        self.tiepoint = t.get(33922)
+        self.geokeys = t.get(34735)
+
+    def _ifd(self, off):
+        d, bo = self._d, self._bo
+        (n,) = struct.unpack(bo + 'H', d[off:off + 2])
+        tags = {}
+        for i in range(n):
+            tag, typ, cnt, val = struct.unpack(bo + 'HHI4s', d[off + 2 + 12 * i:off + 14 + 12 * i])
+            if typ not in _TYPES:
+                continue
+            code, size = _TYPES[typ]
+            nbytes = size * cnt
+            raw = val[:nbytes] if nbytes <= 4 else d[struct.unpack(bo + 'I', val)[0]:][:nbytes]
+            if typ == 2:
+                tags[tag] = raw.decode('latin-1')
+            elif typ in (5, 10):
+                v = struct.unpack(bo + code[0] * (2 * cnt), raw)
+                tags[tag] = tuple(v[k] / v[k + 1] for k in range(0, len(v), 2))
+            else:
+                tags[tag] = struct.unpack(bo + code * cnt, raw)
+        return tags
+
+    def read(self):
+        """All bands as a [bands, rows, cols] array in the sample type (native byte order)."""
+        t, d = self.tags, self._d
+        item = self.dtype.itemsize
+        if 273 in t:  # strips
+            offs, counts = t[273], t[279]
+            raw = b''.join(d[o:o + c] for o, c in zip(offs, counts))
+            if self.planar == 1:
+                a = np.frombuffer(raw, self.dtype, self.width * self.height * self.bands)
+                a = a.reshape(self.height, self.width, self.bands).transpose(2, 0, 1)
+            else:
+                a = np.frombuffer(raw, self.dtype, self.width * self.height * self.bands)
+                a = a.reshape(self.bands, self.height, self.width)
+        elif 324 in t:  # tiles
+            tw, th = int(t[322][0]), int(t[323][0])
+            offs = t[324]
+            tx, ty = -(-self.width // tw), -(-self.height // th)
+            per_band = tx * ty
+            a = np.empty((self.bands, ty * th, tx * tw), self.dtype)
+            for k, o in enumerate(offs):
+                spp = self.bands if self.planar == 1 else 1
+                tile = np.frombuffer(d[o:o + tw * th * spp * item], self.dtype, tw * th * spp)
+                b0 = 0 if self.planar == 1 else k // per_band
+                r = k % per_band
+                yy, xx = (r // tx) * th, (r % tx) * tw
+                if self.planar == 1:
+                    a[:, yy:yy + th, xx:xx + tw] = tile.reshape(th, tw, spp).transpose(2, 0, 1)
+                else:
+                    a[b0, yy:yy + th, xx:xx + tw] = tile.reshape(th, tw)
+            a = a[:, :self.height, :self.width]
+        else:
+            raise TiffError('no strip or tile offsets')
+        return np.ascontiguousarray(a).astype(self.dtype.newbyteorder('='), copy=False)
+
+
+def read_bands(path):
+    """[bands, rows, cols] numpy array of a GeoTIFF (GDAL's ReadAsArray per band, stacked)."""
+    return GeoTiff(path).read()

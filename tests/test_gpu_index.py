@@ -1,0 +1,110 @@
+"""Load stage on the GPU: hiprtc-compiled index kernels against the numpy oracle (bit-exact), the
+reference's rast_algebra test on its own TIFF fixture, and int16 bands -> index raster -> analyze
+end to end against the CPU oracle."""
+import os
+import zlib
+
+import numpy as np
+import pytest
+import torch
+
+from land_trendr_amd import index_eqn
+from land_trendr_amd.geotiff import read_bands
+from land_trendr_amd.scene import build_scene, parse_date
+from land_trendr_amd.settings import compile_params
+from oracle import index_oracle
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope='module')
+def engine():
+    from land_trendr_amd.engine import get_engine
+    return get_engine(0)
+
+
+def _bits_equal(a, b):
+    if a.dtype.kind == 'f':
+        ai = a.view(np.int32 if a.itemsize == 4 else np.int64)
+        bi = b.view(np.int32 if b.itemsize == 4 else np.int64)
+        return (ai == bi) | (np.isnan(a) & np.isnan(b))
+    return a == b
+
+
+INT16_EQNS = ['B1 - B2', '(B4 - B3) / (B4 + B3)', 'B1 * 10000', 'B2 + 40000', '(B1 - B2) * 0.5',
+              'B3 // 7 - -B1', '-B1 / 3 + 1000', '(B2 - B1) / (B2 + B1) * 1000.0', 'B1 + 0.5']
+
+
+@pytest.mark.parametrize('eqn', INT16_EQNS)
+def test_index_kernel_int16_vs_numpy(engine, eqn):
+    prog = index_eqn.IndexProgram(eqn, band_dtype=np.int16)
+    fn = engine.compile_index(prog)
+    rng = np.random.default_rng(zlib.crc32(eqn.encode()))
+    K, NB, P = 3, len(prog.bands), 20000
+    b = rng.integers(-32768, 32768, (K, NB, P)).astype(np.int16)
+    b[:, :, :8] = np.array([0, -1, 1, 32767, -32768, 2, -2, 7], np.int16)  # edge values
+    b[0, :, 8:16] = 0  # x / 0 and 0 / 0
+    got = engine.index_tile(fn, torch.from_numpy(b).to(engine.device))
+    torch.cuda.synchronize()
+    got = got.cpu().numpy()
+    for k in range(K):
+        want = index_oracle.evaluate(prog, b[k])
+        same = _bits_equal(want, got[k])
+        assert same.all(), '%s obs %d: %d of %d differ' % (eqn, k, (~same).sum(), P)
+
+
+def test_index_kernel_float32_and_uint16(engine):
+    rng = np.random.default_rng(3)
+    for eqn, bt, ot in [('B1/2', np.float32, np.float32), ('(B1 - B2) / (B1 + B2)', np.float32,
+                                                            np.float32),
+                        ('B1 - B2', np.uint16, np.uint16), ('B2 - B1 * 3', np.uint16, np.int16),
+                        ('B1 // B2', np.float32, np.float32)]:
+        prog = index_eqn.IndexProgram(eqn, band_dtype=bt, out_dtype=ot)
+        fn = engine.compile_index(prog)
+        if np.dtype(bt).kind == 'f':
+            b = (rng.normal(0, 1000, (2, len(prog.bands), 5000))).astype(bt)
+        else:
+            b = rng.integers(0, 65536, (2, len(prog.bands), 5000)).astype(bt)
+        got = engine.index_tile(fn, torch.from_numpy(b).to(engine.device)).cpu().numpy()
+        for k in range(2):
+            same = _bits_equal(index_oracle.evaluate(prog, b[k]), got[k])
+            assert same.all(), '%s: %d differ' % (eqn, (~same).sum())
+
+
+def test_reference_rast_algebra_half_on_fixture_gpu(engine):
+    """utils_test.py:119-125: rast_algebra(template, 'B1/2') sums to half the template."""
+    bands = read_bands(os.path.join(ROOT, 'tests', 'golden', 'files', 'dummy_single_band.tif'))
+    prog = index_eqn.IndexProgram('B1/2', band_dtype=np.float32)
+    fn = engine.compile_index(prog)
+    b = torch.from_numpy(bands.reshape(1, 1, -1).copy()).to(engine.device)
+    alg = engine.index_tile(fn, b).cpu().numpy().reshape(bands.shape[1:])
+    assert np.sum(bands) / 2 == np.sum(alg)
+    assert _bits_equal(index_oracle.evaluate(prog, bands), alg).all()
+
+
+def test_bands_to_index_to_analyze_vs_oracle(engine):
+    """int16 bands (B1 = B2 + index) -> 'B1 - B2' on the GPU -> int16 index raster -> analyze,
+    bit-exact against the CPU oracle on float(index)."""
+    from land_trendr_amd.synth import make_scene
+    from oracle import oracle
+    sc = make_scene(6000, seed=21, n_years=30, k_min=1, k_max=3, mask_prob=0.15,
+                    with_bands=True)
+    meta = build_scene(sc.dates, parse_date('2014-07-01'))
+    params, _ = compile_params(10.0, [{'name': 'gd', 'val': 1, 'change_type': 'GD'}])
+    prog = index_eqn.IndexProgram('B1 - B2', band_dtype=np.int16)
+    fn = engine.compile_index(prog)
+    dev = engine.device
+    index = engine.index_tile(fn, sc.bands.to(dev))
+    assert index.dtype == torch.int16
+    valid = sc.valid.to(dev)
+    out = engine.analyze_tile(meta, params, index, valid)
+    torch.cuda.synchronize()
+    got = {k: t.cpu().numpy() for k, t in out.items()}
+    vals = index.cpu().numpy().astype(np.float64)
+    assert (vals == sc.values.numpy()).all()
+    want = oracle.analyze_tile(meta, params, vals, sc.valid.numpy(),
+                               n_threads=os.cpu_count() or 1)
+    for f in want:
+        same = _bits_equal(want[f], got[f])
+        assert same.all(), '%s: %d differ' % (f, (~same).sum())
