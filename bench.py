@@ -55,8 +55,8 @@ def f_ref(n):
     return 20 * s3 + n * (n + 1) + 24 * n
 
 
-def bytes_per_pixel(cfg, n_obs, n_years):
-    inp = n_obs * 8 + (n_obs if cfg['mask'] > 0 else 0)          # f64 index values + mask
+def bytes_per_pixel(cfg, n_obs, n_years, value_bytes=8):
+    inp = n_obs * value_bytes + (n_obs if cfg['mask'] > 0 else 0)  # index values + mask
     lab = len(cfg['rules']) * (1 + 4 + 4 + 4 + 8)                 # matched/class/onset/dur/mag
     tl = n_years * (6 * 8 + 2 + 2) if cfg['trendline'] else 0     # 6 f64 + spike/vertex + winner
     return inp + lab + tl + 4                                     # + status
@@ -65,13 +65,15 @@ def bytes_per_pixel(cfg, n_obs, n_years):
 PMC_SUMMARY = os.path.join(ROOT, 'profiles', 'r01_pmc_c2.json')
 
 
-def pmc_traffic(kernel, px_per_launch):
+def pmc_traffic(kernel, px_per_launch, input_mode):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc summary of this build
     (FETCH_SIZE/WRITE_SIZE passes, gfx950-corrected: profiles/summarize_pmc.py), scaled to this
     launch's pixel count; None when absent."""
     try:
         with open(PMC_SUMMARY) as f:
             d = json.load(f)
+        if d.get('_input', 'index') != input_mode:
+            return None
         return d[kernel]['hbm_bytes'] / d['_pixels_per_launch'] * px_per_launch
     except (OSError, KeyError, ValueError, TypeError, ZeroDivisionError):
         return None
@@ -118,6 +120,9 @@ def main():
                     help='N>1: skip the RCCL gather of label rasters to rank 0')
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--input', default='bands', choices=['bands', 'index'],
+                    help='bands: int16 B1, B2 planes + index_eqn "B1 - B2" on the GPU (the '
+                         'reference pipeline, SURVEY.md 8(d)); index: float64 index values')
     args = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -132,11 +137,21 @@ def main():
     P = args.pixels or cfg['pixels']
     dev = torch.device('cuda', local)
 
+    bands_in = args.input == 'bands'
     sc = make_scene(P, n_years=cfg['years'], k_min=cfg['k'][0], k_max=cfg['k'][1],
-                    mask_prob=cfg['mask'], seed=1000 + rank, device=dev)
+                    mask_prob=cfg['mask'], seed=1000 + rank, device=dev, with_bands=bands_in)
+    index_fn = index_buf = None
+    if bands_in:  # the load stage: settings.json index_eqn on int16 bands, compiled with hiprtc
+        from land_trendr_amd.index_eqn import IndexProgram
+        sc.values = None  # only the bands travel
+        torch.cuda.empty_cache()
     meta = build_scene(sc.dates, parse_date('2014-07-01'))
     params, rules = compile_params(cfg['line_cost'], cfg['rules'], cfg['mode'])
     eng = get_engine(local)
+    if bands_in:
+        index_fn = eng.compile_index(IndexProgram('B1 - B2', band_dtype='int16'))
+        index_buf = torch.empty((meta.n_obs, args.tile), dtype=torch.int16, device=dev)
+    idx_events = []
     fields = ['status', 'matched', 'class_val', 'onset_year', 'duration', 'magnitude']
     if cfg['trendline']:
         fields += ['winner', 'val_raw', 'val_fit', 'fit_m', 'fit_b', 'right_m', 'right_b',
@@ -148,10 +163,23 @@ def main():
     if gather and rank == 0:  # the writer's label rasters for the whole job, allocated once
         recv = {f: [torch.empty_like(out[f]) for _ in range(world)] for f in LABEL_GATHER_FIELDS}
 
-    def step():
+    def step(timed=False):
         for p0, p1 in tiles:
             view = {f: (t[..., p0:p1]) for f, t in out.items()}
-            eng.analyze_tile(meta, params, sc.values[:, p0:p1],
+            if bands_in:
+                e0 = e1 = None
+                if timed:
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(
+                        enable_timing=True)
+                    e0.record()
+                values = eng.index_tile(index_fn, sc.bands[:, :, p0:p1],
+                                        out=index_buf[:, :p1 - p0])
+                if timed:
+                    e1.record()
+                    idx_events.append((e0, e1))
+            else:
+                values = sc.values[:, p0:p1]
+            eng.analyze_tile(meta, params, values,
                              sc.valid[:, p0:p1] if sc.valid is not None else None,
                              fields, out=view)
         if gather:  # one RCCL gather per label raster to the writer rank
@@ -168,7 +196,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        step(timed=True)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if dist is not None:
@@ -192,9 +220,11 @@ def main():
     px_per_launch = P * args.steps / n_launch
     flops = f_ref(cfg['years']) * px_per_launch
     achieved = flops / (kern_ms * 1e-3) / 1e12
-    bpp = bytes_per_pixel(cfg, meta.n_obs, meta.n_years)
+    bpp = bytes_per_pixel(cfg, meta.n_obs, meta.n_years, 2 if bands_in else 8)
+    index_ms = (sum(a.elapsed_time(b) for a, b in idx_events) / max(1, len(idx_events))
+                if idx_events else None)
     hbm_gbs = bpp * px_per_launch / (kern_ms * 1e-3) / 1e9
-    traffic = pmc_traffic('analyze', px_per_launch) if args.config == 'c2' else None
+    traffic = pmc_traffic('analyze', px_per_launch, args.input) if args.config == 'c2' else None
     res = {
         'metric': 'Mpixels/sec full analyze (30-yr series)' if cfg['years'] == 30 else
                   'Mpixels/sec full analyze (%d-yr series)' % cfg['years'],
@@ -205,6 +235,8 @@ def main():
         'config': {'workload': cfg['desc'], 'pixels_per_gpu': P, 'years': cfg['years'],
                    'obs': meta.n_obs, 'rules': len(rules), 'line_cost': cfg['line_cost'],
                    'tile_pixels': args.tile, 'gather': bool(gather),
+                   'input': ('int16 bands B1, B2 + index_eqn "B1 - B2"' if bands_in else
+                             'float64 index values'),
                    'parallelism': 'pixel tiles, 1 scene per GPU'},
         # dominant kernel: the analyze stage, FP64-VALU bound (O(n^2) DP per 240-byte series).
         # achieved = the reference algorithm's flops (F_ref) per launch / the
@@ -221,6 +253,11 @@ def main():
                      'hbm': {'achieved': round(hbm_gbs, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                              'frac': round(hbm_gbs / HBM_PEAK_GBS, 4)}},
         'status_numeric_pixels': n_numeric,
+        'load_stage': None if index_ms is None else {
+            'kernel': 'lt_index_kernel (hiprtc, index_eqn "B1 - B2", int16 bands -> int16)',
+            'ms_per_launch': round(index_ms, 3),
+            'hbm_gbs_algorithmic': round(meta.n_obs * 6 * px_per_launch / (index_ms * 1e-3) / 1e9,
+                                         1)},
         'resolve_stage': {'ms_per_launch': round(resolve_ms, 3),
                           'deferred_pixels_last_tile': n_deferred_last,
                           'last_tile_pixels': tiles[-1][1] - tiles[-1][0]},

@@ -477,7 +477,8 @@ int lt_index_compile(lt_ctx* c, const lt_index_prog* prog, lt_index** out) {
   f->band_type = prog->band_type;
   f->out_type = prog->out_type;
   if (hipModuleLoadData(&f->mod, code.data()) != hipSuccess ||
-      hipModuleGetFunction(&f->fn, f->mod, "lt_index_kernel") != hipSuccess) {
+      hipModuleGetFunction(&f->fn, f->mod, "lt_index_kernel") != hipSuccess ||
+      hipModuleGetFunction(&f->fn4, f->mod, "lt_index_kernel4") != hipSuccess) {
     if (f->mod) (void)hipModuleUnload(f->mod);
     delete f;
     return fail(c, LT_ERR_JIT, "module load failed%s");
@@ -497,13 +498,31 @@ int lt_index_apply(lt_ctx* c, const lt_index* f, const lt_index_io* io, void* st
       io->obs_stride < (int64_t)f->n_bands * io->band_stride)
     return fail(c, LT_ERR_ARG, "bad strides%s");
   HIP_OR_FAIL(c, hipSetDevice(c->device));
-  const void* bands = io->bands;
-  void* outp = io->out;
-  long long obs_stride = io->obs_stride, band_stride = io->band_stride, n_pix = io->n_pix,
+  long long obs_stride = io->obs_stride, band_stride = io->band_stride,
             out_stride = io->out_stride;
-  void* args[] = {(void*)&bands, &obs_stride, &band_stride, &n_pix, &outp, &out_stride};
-  const unsigned gx = (unsigned)((io->n_pix + 255) / 256);
-  HIP_OR_FAIL(c, hipModuleLaunchKernel(f->fn, gx, (unsigned)io->n_obs, 1, 256, 1, 1, 0,
-                                       (hipStream_t)stream_, args, nullptr));
+  const size_t bsz = lt_idx::type_size(f->band_type), osz = lt_idx::type_size(f->out_type);
+  // 4-pixel vector kernel over the 4-aligned head when every plane start is 4-element aligned
+  const bool vec_ok = ((uintptr_t)io->bands % (4 * bsz)) == 0 &&
+                      ((uintptr_t)io->out % (4 * osz)) == 0 && obs_stride % 4 == 0 &&
+                      band_stride % 4 == 0 && out_stride % 4 == 0;
+  const long long head = vec_ok ? (io->n_pix & ~3LL) : 0;
+  if (head > 0) {
+    const void* bands = io->bands;
+    void* outp = io->out;
+    long long n_pix = head;
+    void* args[] = {(void*)&bands, &obs_stride, &band_stride, &n_pix, &outp, &out_stride};
+    const unsigned gx = (unsigned)((head / 4 + 255) / 256);
+    HIP_OR_FAIL(c, hipModuleLaunchKernel(f->fn4, gx, (unsigned)io->n_obs, 1, 256, 1, 1, 0,
+                                         (hipStream_t)stream_, args, nullptr));
+  }
+  if (head < io->n_pix) {
+    const void* bands = (const char*)io->bands + head * bsz;
+    void* outp = (char*)io->out + head * osz;
+    long long n_pix = io->n_pix - head;
+    void* args[] = {(void*)&bands, &obs_stride, &band_stride, &n_pix, &outp, &out_stride};
+    const unsigned gx = (unsigned)((n_pix + 255) / 256);
+    HIP_OR_FAIL(c, hipModuleLaunchKernel(f->fn, gx, (unsigned)io->n_obs, 1, 256, 1, 1, 0,
+                                         (hipStream_t)stream_, args, nullptr));
+  }
   return LT_OK;
 }

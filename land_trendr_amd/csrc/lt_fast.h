@@ -105,9 +105,29 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
       }
     }
     double val[WB];
+    // unconditional loads (obs 0 / pixel 0 stand in), one typed batch per launch-uniform type:
+    // all WB loads in flight at once
+    auto batch = [&](auto tag) {
+      using T = decltype(tag);
+      const T* base = in.obs_index ? (const T*)in.obs_index : (const T*)in.obs_val;
+      T raw[WB];
 #pragma unroll
-    for (int u = 0; u < WB; u++)  // unconditional (obs 0 / pixel 0 stand in): all in flight
-      val[u] = obs_value(in, (int64_t)(best[u] >= 0 ? best[u] : 0) * is + (live ? p : 0));
+      for (int u = 0; u < WB; u++)
+        raw[u] = base[(int64_t)(best[u] >= 0 ? best[u] : 0) * is + (live ? p : 0)];
+#pragma unroll
+      for (int u = 0; u < WB; u++) val[u] = (double)raw[u];
+    };
+    if (in.obs_index == nullptr) batch(double{});
+    else if (in.index_type == LT_T_I16) batch(int16_t{});
+    else if (in.index_type == LT_T_F32) batch(float{});
+    else if (in.index_type == LT_T_U16) batch(uint16_t{});
+    else if (in.index_type == LT_T_I32) batch(int32_t{});
+    else if (in.index_type == LT_T_U8) batch(uint8_t{});
+    else {
+#pragma unroll
+      for (int u = 0; u < WB; u++)
+        val[u] = obs_value(in, (int64_t)(best[u] >= 0 ? best[u] : 0) * is + (live ? p : 0));
+    }
 #pragma unroll
     for (int u = 0; u < WB; u++) {
       const int y = yb + u;

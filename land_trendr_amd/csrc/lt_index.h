@@ -16,7 +16,7 @@
 
 struct lt_index {
   hipModule_t mod = nullptr;
-  hipFunction_t fn = nullptr;
+  hipFunction_t fn = nullptr, fn4 = nullptr;
   int32_t n_bands = 0, band_type = 0, out_type = 0;
 };
 
@@ -37,6 +37,14 @@ inline const char* ctype(int t) {
   }
 }
 inline bool is_float(int t) { return t == LT_T_F64 || t == LT_T_F32; }
+inline size_t type_size(int t) {
+  switch (t) {
+    case LT_T_F64: case LT_T_I64: return 8;
+    case LT_T_I32: case LT_T_F32: case LT_T_U32: return 4;
+    case LT_T_I16: case LT_T_U16: return 2;
+    default: return 1;
+  }
+}
 inline bool is_unsigned(int t) { return t == LT_T_U16 || t == LT_T_U8 || t == LT_T_U32; }
 // integer range of a type (for the saturating store)
 inline void int_range(int t, long long& lo, long long& hi) {
@@ -102,8 +110,48 @@ inline std::string fmt_double(double d) {
   return b;
 }
 
-// Generated source for prog, or "" with err set.
+// Generated source for prog, or "" with err set. Two kernels: lt_index_kernel (one pixel per
+// thread) and lt_index_kernel4 (four consecutive pixels per thread, vector loads and stores, for
+// 4-aligned planes; the host sends the tail to the scalar one).
+inline std::string codegen_body(const lt_index_prog& P, bool vec, std::string& err,
+                                std::string& store_out);
 inline std::string codegen(const lt_index_prog& P, std::string& err) {
+  std::string store1, store4;
+  const std::string body1 = codegen_body(P, false, err, store1);
+  if (body1.empty()) return "";
+  const std::string body4 = codegen_body(P, true, err, store4);
+  const char* BT = ctype(P.band_type);
+  const char* OT = ctype(P.out_type);
+  std::string src = kPrelude;
+  src += std::string("typedef ") + BT + " lt_bt4 __attribute__((ext_vector_type(4)));\n";
+  src += std::string("typedef ") + OT + " lt_ot4 __attribute__((ext_vector_type(4)));\n";
+  src += std::string("extern \"C\" __global__ __launch_bounds__(256) void lt_index_kernel(const ") +
+         BT + "* __restrict__ bands, long long obs_stride, long long band_stride, long long n_pix, " +
+         OT + "* __restrict__ out, long long out_stride) {\n"
+         "  const long long p = (long long)blockIdx.x * 256 + threadIdx.x;\n"
+         "  const long long o = blockIdx.y;\n"
+         "  if (p >= n_pix) return;\n"
+         "  const " + BT + "* b = bands + o * obs_stride + p;\n";
+  src += body1;
+  src += "  out[o * out_stride + p] = " + store1 + ";\n}\n";
+  src += std::string("extern \"C\" __global__ __launch_bounds__(256) void lt_index_kernel4(const ") +
+         BT + "* __restrict__ bands, long long obs_stride, long long band_stride, long long n_pix, " +
+         OT + "* __restrict__ out, long long out_stride) {\n"
+         "  const long long p = ((long long)blockIdx.x * 256 + threadIdx.x) * 4;\n"
+         "  const long long o = blockIdx.y;\n"
+         "  if (p >= n_pix) return;\n"
+         "  const " + BT + "* b = bands + o * obs_stride + p;\n";
+  for (int s = 0; s < P.n_bands; s++)
+    src += "  const lt_bt4 bv" + std::to_string(s) + " = *(const lt_bt4*)(b + " +
+           std::to_string(s) + "LL * band_stride);\n";
+  src += "  lt_ot4 res;\n#pragma unroll\n  for (int j = 0; j < 4; j++) {\n";
+  src += body4;
+  src += "  res[j] = " + store4 + ";\n  }\n  *(lt_ot4*)(out + o * out_stride + p) = res;\n}\n";
+  return src;
+}
+
+inline std::string codegen_body(const lt_index_prog& P, bool vec, std::string& err,
+                                std::string& store_out) {
   if (P.n_ops < 1 || P.n_ops > LT_MAX_PROG || P.n_bands < 1 || P.n_bands > LT_MAX_BANDS ||
       !ctype(P.band_type) || !ctype(P.out_type)) {
     err = "index program: bad sizes or types";
@@ -126,8 +174,12 @@ inline std::string codegen(const lt_index_prog& P, std::string& err) {
           err = "index program: bad band slot";
           return "";
         }
-        snprintf(line, sizeof line, "  const %s %s = b[%lldLL * band_stride];\n", T, v.c_str(),
-                 (long long)o.ival);
+        if (vec)
+          snprintf(line, sizeof line, "  const %s %s = bv%lld[j];\n", T, v.c_str(),
+                   (long long)o.ival);
+        else
+          snprintf(line, sizeof line, "  const %s %s = b[%lldLL * band_stride];\n", T, v.c_str(),
+                   (long long)o.ival);
         body += line;
         st.push_back({v, o.type});
         break;
@@ -231,18 +283,8 @@ inline std::string codegen(const lt_index_prog& P, std::string& err) {
     }
     store = b;
   }
-  std::string src = kPrelude;
-  src += std::string("extern \"C\" __global__ __launch_bounds__(256) void lt_index_kernel(const ") +
-         ctype(P.band_type) +
-         "* __restrict__ bands, long long obs_stride, long long band_stride, long long n_pix, " +
-         OT + "* __restrict__ out, long long out_stride) {\n"
-         "  const long long p = (long long)blockIdx.x * 256 + threadIdx.x;\n"
-         "  const long long o = blockIdx.y;\n"
-         "  if (p >= n_pix) return;\n"
-         "  const " + ctype(P.band_type) + "* b = bands + o * obs_stride + p;\n";
-  src += body;
-  src += "  out[o * out_stride + p] = " + store + ";\n}\n";
-  return src;
+  store_out = store;
+  return body;
 }
 
 }  // namespace lt_idx
