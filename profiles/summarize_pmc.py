@@ -1,6 +1,6 @@
 """Summarise rocprofv3 --pmc CSV passes into per-launch numbers for the engine's kernels.
 
-Usage: python profiles/summarize_pmc.py <pmc_root> <out.json> [pixels_per_launch]
+Usage: python profiles/summarize_pmc.py <pmc_root> <out.json> [pixels_per_launch] [input]
 <pmc_root> holds one sub-directory per pass (run_counter_collection.csv in each), as written by
 profiles/pmc_passes.sh. HBM traffic follows MI355X_MICROARCH.md §HBM: FETCH_SIZE/WRITE_SIZE are
 in KB; on gfx950 FETCH_SIZE reports half of the bytes of a coalesced streaming read, so it is
@@ -15,13 +15,14 @@ import os
 import sys
 
 
-def main(root, out, px=None):
+def main(root, out, px=None, input_mode='bands'):
     per = collections.defaultdict(lambda: collections.defaultdict(float))
     launches = collections.defaultdict(set)
     for f in glob.glob(os.path.join(root, '*', 'run_counter_collection.csv')):
         for r in csv.DictReader(open(f)):
             k = r['Kernel_Name']
-            name = ('analyze' if 'analyze' in k else 'resolve' if 'resolve' in k else None)
+            name = ('analyze' if 'analyze' in k else 'resolve' if 'resolve' in k else
+                    'index' if 'lt_index_kernel' in k else None)
             if name is None:
                 continue
             per[name][r['Counter_Name']] += float(r['Counter_Value'])
@@ -42,9 +43,11 @@ def main(root, out, px=None):
         res[name] = row
     res['_source'] = root
     res['_pixels_per_launch'] = px
+    res['_input'] = input_mode
     json.dump(res, open(out, 'w'), indent=1, sort_keys=True)
     print(json.dumps(res, indent=1, sort_keys=True))
 
 
 if __name__ == '__main__':
-    main(sys.argv[1], sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else None)
+    main(sys.argv[1], sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else None,
+         sys.argv[4] if len(sys.argv) > 4 else 'bands')
