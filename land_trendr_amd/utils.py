@@ -21,7 +21,7 @@ from .scene import build_scene, parse_date
 from .settings import compile_params, load_settings
 
 __all__ = ['parse_date', 'analyze', 'change_labeling', 'analysis_reducer',
-           'analysis_reducer_batch', 'analyze_tile', 'match_rules_gpu']
+           'analysis_reducer_batch', 'analyze_tile', 'index_tile', 'match_rules_gpu']
 
 
 def _raise_for_status(status, n_obs_valid):
@@ -129,16 +129,39 @@ def analysis_reducer(point_wkt, pix_datas, settings, pre_threshold_mode='referen
 
 
 def analysis_reducer_batch(dates, values, valid, settings, fields=LABELS + ('status',),
-                           pre_threshold_mode='reference', device=None):
-    """Batched analysis_reducer: a co-registered tile (obs `dates`, values [K, P] float64,
-    valid [K, P] uint8 or None, on the GPU) -> dict of dense output planes (GPU tensors):
-    the label rasters the reference emits per grid point as '<label>_<field>' values, and,
-    when requested, the trendline planes ('trendline/<date>-<attr>' values, per year slot)."""
+                           pre_threshold_mode='reference', device=None, bands=None,
+                           band_numbers=None):
+    """Batched analysis_reducer: a co-registered tile (obs `dates`, values [K, P] — float64 or
+    an index raster in its stored type — valid [K, P] uint8 or None, on the GPU) -> dict of dense
+    output planes (GPU tensors): the label rasters the reference emits per grid point as
+    '<label>_<field>' values, and, when requested, the trendline planes
+    ('trendline/<date>-<attr>' values, per year slot).
+
+    bands: instead of values, the raw band planes [K, n_bands, P] (their dtype is the raster's);
+    settings['index_eqn'] is then evaluated on the GPU first (parse_mapper's rast_algebra,
+    mr_land_trendr_job.py:67-68). band_numbers: the reference band number of each plane (default
+    1..n_bands)."""
     settings = load_settings(settings)
     scene = build_scene(dates, parse_date(settings['target_date']))
     params, rules = compile_params(settings['line_cost'], settings.get('label_rules', ()),
                                    pre_threshold_mode)
+    if bands is not None:
+        values = index_tile(settings['index_eqn'], bands, band_numbers, device=device)
     out = analyze_tile(scene, params, values, valid, fields, device=device)
     out['_scene'] = scene
     out['_rules'] = rules
     return out
+
+
+def index_tile(index_eqn, bands, band_numbers=None, device=None):
+    """rast_algebra (utils.py:447-484) on the GPU: bands [K, n_bands, P] (the raster's dtype) ->
+    the index raster [K, P] in the same dtype (array2raster's template type, utils.py:396-397)."""
+    from .index_eqn import IndexProgram
+    eng = get_engine(device)
+    nb = bands.shape[1]
+    numbers = list(band_numbers) if band_numbers is not None else list(range(1, nb + 1))
+    prog = IndexProgram(index_eqn, band_dtype=np.dtype(str(bands.dtype).replace('torch.', '')),
+                        raster_count=max(numbers))
+    slots = [numbers.index(b) for b in prog.bands]  # the planes the equation reads, in order
+    sel = bands[:, slots, :] if slots != list(range(nb)) else bands
+    return eng.index_tile(eng.compile_index(prog), sel.contiguous() if sel.stride(2) != 1 else sel)

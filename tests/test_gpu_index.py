@@ -108,3 +108,22 @@ def test_bands_to_index_to_analyze_vs_oracle(engine):
     for f in want:
         same = _bits_equal(want[f], got[f])
         assert same.all(), '%s: %d differ' % (f, (~same).sum())
+
+
+def test_analysis_reducer_batch_from_bands(engine):
+    """The batched reducer fed raw band planes (index_eqn on the GPU) equals the one fed the
+    index values; extra unused planes are skipped by band number."""
+    from land_trendr_amd.synth import make_scene
+    from land_trendr_amd.utils import analysis_reducer_batch
+    sc = make_scene(3000, seed=5, n_years=25, with_bands=True)
+    dev = engine.device
+    settings = {'line_cost': 10, 'target_date': '2014-07-01', 'index_eqn': 'B4 - B2',
+                'label_rules': [{'name': 'gd', 'val': 1, 'change_type': 'GD'}]}
+    K, _, P = sc.bands.shape
+    junk = torch.zeros((K, 1, P), dtype=torch.int16)
+    planes = torch.cat([junk, sc.bands[:, 1:2], junk, sc.bands[:, 0:1]], dim=1).to(dev)
+    a = analysis_reducer_batch(sc.dates, None, None, settings, bands=planes,
+                               band_numbers=[1, 2, 3, 4])
+    b = analysis_reducer_batch(sc.dates, sc.values.to(dev), None, settings)
+    for f in ('status', 'matched', 'class_val', 'onset_year', 'duration', 'magnitude'):
+        assert torch.equal(a[f], b[f]), f
