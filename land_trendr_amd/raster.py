@@ -1,0 +1,209 @@
+"""Output raster assembly: MRLandTrendrJob.output_reducer
+(mr_land_trendr_job.py:128-152) -> utils.data2raster (utils.py:414-440) -> utils.array2raster
+(:374-412), for the dense label / trendline planes the GPU produces.
+
+The reference fills, per output key, a holder shaped like the template raster's band 1 with
+`np.ones_like(ds2array(template)) * NODATA` (so in the template's dtype), assigns
+`float(value)` at each grid point's pixel (numpy's cast into that dtype: truncation toward zero
+for integer templates), and writes it with `array2raster(holder, template_fn, out_fn, compress)`
+— whose fourth positional parameter is `data_type`, so `compress=True` becomes GDAL type 1,
+GDT_Byte. GDAL then saturates every value into 0..255 (-99 -> 0,
+1995 -> 255). Two modes:
+
+  * 'reference': that behaviour (uint8 rasters) — parity with what the reference writes, where
+    GDAL's saturating Int->Byte/Float->Byte conversion is restated (GDAL absent here: unpinned);
+  * 'typed': the corrected output — each field in its own type (int32 class/onset/duration,
+    float64 magnitude), NODATA -99 where a rule did not match.
+
+Keys follow the reference: '<rule>_<field>' for labels (mr_land_trendr_job.py:120-126) and
+'trendline/<YYYY-MM-DD>-<attr>' per winning acquisition date for the trendline planes
+(classes.py:100-116). Files are written by write_geotiff: uncompressed GeoTIFF with the template's
+georeferencing tags copied (the reference asks GDAL for LZW: a storage detail, values equal).
+"""
+import struct
+
+import numpy as np
+
+from . import _abi
+from .geotiff import GeoTiff
+
+NODATA = _abi.LT_NODATA  # settings.py:16
+LABEL_KEYS = ('class_val', 'onset_year', 'magnitude', 'duration')
+TRENDLINE_ATTRS = ('val_raw', 'val_fit', 'eqn_fit_slope', 'eqn_fit_intercept', 'eqn_right_slope',
+                   'eqn_right_intercept', 'spike', 'vertex')
+_PLANE_OF_ATTR = {'val_raw': 'val_raw', 'val_fit': 'val_fit', 'eqn_fit_slope': 'fit_m',
+                  'eqn_fit_intercept': 'fit_b', 'eqn_right_slope': 'right_m',
+                  'eqn_right_intercept': 'right_b', 'spike': 'spike', 'vertex': 'vertex'}
+
+
+def _holder_cast(values, template_dtype):
+    """numpy's assignment of float(value) into the holder's dtype (utils.py:433-438)."""
+    v = np.asarray(values, np.float64)
+    t = np.dtype(template_dtype)
+    if t.kind == 'f':
+        return v.astype(t)
+    with np.errstate(invalid='ignore'):
+        return np.trunc(v).astype(np.int64).astype(t)  # C cast: toward zero, then wrap
+
+
+def gdal_to_byte(a):
+    """GDAL's conversion of a holder into a GDT_Byte band: round (floats) and saturate."""
+    a = np.asarray(a)
+    if a.dtype.kind == 'f':
+        a = np.where(np.isnan(a), 0.0, np.floor(a + 0.5))
+    return np.clip(a, 0, 255).astype(np.uint8)
+
+
+def label_rasters(out, rules, shape, template_dtype=np.int16, mode='reference'):
+    """Dense label planes of one analysed tile (Engine.analyze_tile output, host or device
+    tensors, [R, P] with P = rows * cols of `shape`) -> {'<rule>_<field>': 2-D array}.
+    Pixels whose rule did not match hold NODATA, as the reference's holder does."""
+    rows, cols = shape
+    res = {}
+    matched = _np(out['matched'])
+    for r, rule in enumerate(rules):
+        m = matched[r, :rows * cols].reshape(rows, cols).astype(bool)
+        for key in LABEL_KEYS:
+            plane = _np(out[key])[r, :rows * cols].reshape(rows, cols)
+            if key == 'class_val':
+                plane = np.full(plane.shape, rule.val, np.int32)
+            if mode == 'typed':
+                typ = np.float64 if key == 'magnitude' else np.int32
+                res['%s_%s' % (rule.name, key)] = np.where(m, plane, NODATA).astype(typ)
+            else:
+                holder = np.full((rows, cols), NODATA, np.int64).astype(template_dtype)
+                holder[m] = _holder_cast(plane[m], template_dtype)
+                res['%s_%s' % (rule.name, key)] = gdal_to_byte(holder)
+    return res
+
+
+def trendline_rasters(out, scene, dates, shape, template_dtype=np.int16, mode='reference',
+                      attrs=TRENDLINE_ATTRS):
+    """Per winning acquisition date d and attribute a, the raster 'trendline/<d>-<a>': the pixels
+    whose winner in d's year is d carry the attribute, all others NODATA (the reference's
+    mr_label_output keys, classes.py:100-116, reduced per key)."""
+    rows, cols = shape
+    n = rows * cols
+    winner = _np(out['winner'])
+    res = {}
+    for y in range(scene.n_years):
+        w = winner[y, :n].reshape(rows, cols)
+        for o in np.unique(w[w >= 0]):
+            d = dates[int(o)].strftime('%Y-%m-%d')
+            sel = w == o
+            for a in attrs:
+                plane = _np(out[_PLANE_OF_ATTR[a]])[y, :n].reshape(rows, cols)
+                if a in ('spike', 'vertex'):
+                    plane = plane.astype(np.int64)  # mr_label_output emits 1 / 0 (classes.py:107)
+                key = 'trendline/%s-%s' % (d, a)
+                if mode == 'typed':
+                    typ = np.uint8 if a in ('spike', 'vertex') else np.float64
+                    r = np.full((rows, cols), NODATA, np.float64)
+                    r[sel] = plane[sel]
+                    res[key] = r.astype(typ) if typ != np.uint8 else np.where(sel, plane, 0).astype(
+                        np.uint8)
+                else:
+                    holder = np.full((rows, cols), NODATA, np.int64).astype(template_dtype)
+                    holder[sel] = _holder_cast(plane[sel], template_dtype)
+                    res[key] = gdal_to_byte(holder)
+    return res
+
+
+def _np(t):
+    try:
+        import torch
+        if isinstance(t, torch.Tensor):
+            return t.detach().cpu().numpy()
+    except ImportError:
+        pass
+    return np.asarray(t)
+
+
+# ---- GeoTIFF writer ----------------------------------------------------------------------------
+_SAMPLE_FORMAT = {'u': 1, 'i': 2, 'f': 3}
+_GEO_TAGS = (33550, 33922, 34264, 34735, 34736, 34737)  # scale, tiepoint, transform, geokeys ...
+
+
+def write_geotiff(path, array, template=None, nodata=NODATA):
+    """Single-band, uncompressed, little-endian GeoTIFF of a 2-D array; georeferencing tags copied
+    verbatim from `template` (a GeoTiff or a path), GDAL_NODATA set to `nodata`."""
+    a = np.ascontiguousarray(array)
+    if a.ndim != 2 or a.dtype.kind not in _SAMPLE_FORMAT:
+        raise ValueError('write_geotiff: 2-D integer or float array required')
+    a = a.astype(a.dtype.newbyteorder('<'), copy=False)
+    rows, cols = a.shape
+    tmpl = GeoTiff(template) if isinstance(template, str) else template
+    entries = []  # (tag, type, count, payload bytes)
+
+    def add(tag, typ, values, fmt):
+        payload = struct.pack('<' + fmt * len(values), *values)
+        entries.append((tag, typ, len(values), payload))
+
+    add(256, 4, [cols], 'I')
+    add(257, 4, [rows], 'I')
+    add(258, 3, [a.dtype.itemsize * 8], 'H')
+    add(259, 3, [1], 'H')
+    add(262, 3, [1], 'H')
+    data = a.tobytes()
+    add(273, 4, [0], 'I')  # patched below
+    add(277, 3, [1], 'H')
+    add(278, 4, [rows], 'I')
+    add(279, 4, [len(data)], 'I')
+    add(284, 3, [1], 'H')
+    add(339, 3, [_SAMPLE_FORMAT[a.dtype.kind]], 'H')
+    if tmpl is not None:
+        for tag in _GEO_TAGS:
+            if tag in tmpl.tags:
+                v = tmpl.tags[tag]
+                if isinstance(v, str):
+                    entries.append((tag, 2, len(v), v.encode('latin-1')))
+                elif tag == 34735:
+                    add(tag, 3, [int(x) for x in v], 'H')
+                else:
+                    add(tag, 12, [float(x) for x in v], 'd')
+    if nodata is not None:
+        s = ('%g' % nodata).encode() + b'\x00'
+        entries.append((42113, 2, len(s), s))
+    entries.sort(key=lambda e: e[0])
+    n = len(entries)
+    ifd_off = 8
+    extra_off = ifd_off + 2 + 12 * n + 4
+    extra = b''
+    ifd = struct.pack('<H', n)
+    offsets = {}
+    for tag, typ, cnt, payload in entries:
+        if len(payload) <= 4:
+            ifd += struct.pack('<HHI', tag, typ, cnt) + payload.ljust(4, b'\x00')
+        else:
+            if len(extra) % 2:
+                extra += b'\x00'
+            offsets[tag] = extra_off + len(extra)
+            ifd += struct.pack('<HHII', tag, typ, cnt, offsets[tag])
+            extra += payload
+    ifd += struct.pack('<I', 0)
+    data_off = extra_off + len(extra)
+    data_off += (-data_off) % 8
+    # patch StripOffsets (tag 273, inline) with the data offset
+    k = [e[0] for e in entries].index(273)
+    pos = 2 + 12 * k + 8
+    ifd = ifd[:pos] + struct.pack('<I', data_off) + ifd[pos + 4:]
+    with open(path, 'wb') as f:
+        f.write(b'II*\x00' + struct.pack('<I', ifd_off))
+        f.write(ifd)
+        f.write(extra)
+        f.write(b'\x00' * (data_off - extra_off - len(extra)))
+        f.write(data)
+    return path
+
+
+def output_reducer(rasters, template, out_dir, job='job'):
+    """The file side of output_reducer (mr_land_trendr_job.py:128-152) without S3: every key's
+    raster written as <out_dir>/<job>/output/rasters/<key>.tif (settings.py OUT_RAST_KEYNAME) with
+    the template's georeferencing. Yields (key, [path]) like the reducer yields (key, [s3 key])."""
+    import os
+    tmpl = GeoTiff(template) if isinstance(template, str) else template
+    for key in sorted(rasters):
+        path = os.path.join(out_dir, '%s/output/rasters/%s.tif' % (job, key))
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        write_geotiff(path, rasters[key], template=tmpl)
+        yield key, [path]
