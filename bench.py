@@ -7,9 +7,10 @@ synthetic, generated directly in HBM before the timed region.
 
 A step = one pass of the hot path over the rank's whole scene, as a queue of pixel tiles
 (lt_analyze_tile launches on the current stream). Multi-GPU (torchrun, one process per GPU):
-each rank analyses its own scene (weak scaling, no data-path collective), then the label
-rasters are gathered to rank 0 over RCCL inside the step (the reference's output_reducer input,
-SURVEY.md §8(e); --no-gather drops it).
+each rank analyses its own scene (weak scaling, no data-path collective) and gathers each tile's
+label rasters to rank 0 over RCCL inside the step, asynchronously, so the transfer of tile t runs
+while tile t+1 computes (the reference's output_reducer input; --no-gather
+drops it).
 """
 import argparse
 import json
@@ -128,11 +129,18 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    # LT_BENCH_DEVICE / LT_BENCH_BACKEND: rehearsal hooks only (several ranks on one GPU over
+    # gloo, to exercise the N>1 path on a 1-GPU box); the driver's runs use neither
+    local = int(os.environ.get('LT_BENCH_DEVICE', local))
+    backend = os.environ.get('LT_BENCH_BACKEND', 'nccl')
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        else:
+            dist.init_process_group(backend)
     cfg = CONFIGS[args.config]
     P = args.pixels or cfg['pixels']
     dev = torch.device('cuda', local)
@@ -156,16 +164,20 @@ def main():
     if cfg['trendline']:
         fields += ['winner', 'val_raw', 'val_fit', 'fit_m', 'fit_b', 'right_m', 'right_b',
                    'spike', 'vertex']
-    out = eng.alloc_outputs(meta.n_years, params.n_rules, P, fields)
     tiles = [(p0, min(P, p0 + args.tile)) for p0 in range(0, P, args.tile)]
+    # tile-major output planes: tile t's [R|Y, tile] slab of every field is contiguous, so it can
+    # be handed to RCCL as soon as its kernels are queued
+    slabs = [eng.alloc_outputs(meta.n_years, params.n_rules, args.tile, fields) for _ in tiles]
     gather = dist is not None and not args.no_gather
     recv = None
     if gather and rank == 0:  # the writer's label rasters for the whole job, allocated once
-        recv = {f: [torch.empty_like(out[f]) for _ in range(world)] for f in LABEL_GATHER_FIELDS}
+        recv = {f: [[torch.empty_like(sl[f]) for sl in slabs] for _ in range(world)]
+                for f in LABEL_GATHER_FIELDS}
+    works = []
 
     def step(timed=False):
-        for p0, p1 in tiles:
-            view = {f: (t[..., p0:p1]) for f, t in out.items()}
+        for t, (p0, p1) in enumerate(tiles):
+            view = {f: x[..., :p1 - p0] for f, x in slabs[t].items()}
             if bands_in:
                 e0 = e1 = None
                 if timed:
@@ -182,9 +194,14 @@ def main():
             eng.analyze_tile(meta, params, values,
                              sc.valid[:, p0:p1] if sc.valid is not None else None,
                              fields, out=view)
-        if gather:  # one RCCL gather per label raster to the writer rank
-            for f in LABEL_GATHER_FIELDS:
-                dist.gather(out[f], recv[f] if rank == 0 else None, dst=0)
+            if gather:  # this tile's label rasters to the writer rank, on
+                # RCCL's stream: it runs while the next tiles compute
+                for f in LABEL_GATHER_FIELDS:
+                    works.append(dist.gather(
+                        slabs[t][f], [recv[f][r][t] for r in range(world)] if rank == 0 else None,
+                        dst=0, async_op=True))
+        while works:
+            works.pop().wait()
 
     for _ in range(args.warmup):
         step()
@@ -210,7 +227,8 @@ def main():
     elapsed = float(elapsed.item())
 
     # correctness gate on this run's own outputs: no pixel may be flagged as an unemulated path
-    n_numeric = int(((out['status'] & 16) != 0).sum().item())
+    n_numeric = sum(int(((sl['status'][:p1 - p0] & 16) != 0).sum().item())
+                    for sl, (p0, p1) in zip(slabs, tiles))
 
     total_px = P * world * args.steps
     value = total_px / elapsed / 1e6

@@ -41,6 +41,17 @@ __global__ __launch_bounds__(kBlock) void analyze_kernel(const lt::DevScene* __r
   if (deferred) defer[base + __popcll(mask & ((1ull << lane) - 1))] = p;
 }
 
+__device__ inline void defer_append(bool deferred, int64_t p, int lane, int64_t* __restrict__ list,
+                                    unsigned long long* __restrict__ count) {
+  const uint64_t mask = __ballot(deferred);
+  if (mask == 0) return;
+  const int leader = __ffsll((long long)mask) - 1;
+  unsigned long long base = 0;
+  if (lane == leader) base = atomicAdd(count, (unsigned long long)__popcll(mask));
+  base = __shfl(base, leader);
+  if (deferred) list[base + __popcll(mask & ((1ull << lane) - 1))] = p;
+}
+
 // Stage 1 (wave-lockstep body, lt_fast.h): one wave per workgroup, the pixel series in LDS.
 template <int MAXY, int RMAX>
 __global__ __launch_bounds__(64) void analyze_fast_kernel(const lt::DevScene* __restrict__ S,
@@ -53,28 +64,24 @@ __global__ __launch_bounds__(64) void analyze_fast_kernel(const lt::DevScene* __
   const int lane = threadIdx.x;
   const int64_t p = (int64_t)blockIdx.x * 64 + lane;
   const bool live = p < in.n_pix;
-  const bool deferred =
-      !lt::analyze_fast<MAXY, RMAX, false, float>(*S, P, in, out, xtab, p, live, lane, L) && live;
-  const uint64_t mask = __ballot(deferred);
-  if (mask == 0) return;
-  const int leader = __ffsll((long long)mask) - 1;
-  unsigned long long base = 0;
-  if (lane == leader) base = atomicAdd(n_defer, (unsigned long long)__popcll(mask));
-  base = __shfl(base, leader);
-  if (deferred) defer[base + __popcll(mask & ((1ull << lane) - 1))] = p;
+  const int d = lt::analyze_fast<MAXY, RMAX, false, float>(*S, P, in, out, xtab, p, live, lane, L);
+  // two lists: [0, n_pix) for the binary32 resolve, [n_pix, 2 n_pix) for the binary64 one;
+  // counters [0] / [2] count them (wave-aggregated atomics)
+  defer_append(live && d == lt::kDeferExact, p, lane, defer, &n_defer[0]);
+  defer_append(live && d == lt::kDeferWide, p, lane, defer + in.n_pix, &n_defer[2]);
 }
 
 // Stage 2 (wave-lockstep, lt_fast.h with EXACT): the deferred pixels, binary64 series in LDS,
 // exact-OPT DP. A grid of exactly the resident waves takes 64-pixel groups of the list from a
 // counter (group cost varies a lot); every wave leaves once the counter has passed the list.
-template <int MAXY, int RMAX>
+template <int MAXY, int RMAX, class VT>
 __global__ __launch_bounds__(64) void resolve_fast_kernel(const lt::DevScene* __restrict__ S,
                                                           const lt_params P, const lt_tile_in in,
                                                           const lt_tile_out out,
                                                           const lt::lsq_xf* __restrict__ xtab,
                                                           const int64_t* __restrict__ defer,
                                                           unsigned long long* __restrict__ counters) {
-  __shared__ lt::WaveLds<MAXY, double> L;
+  __shared__ lt::WaveLds<MAXY, VT> L;
   const int lane = threadIdx.x;
   const int64_t n = (int64_t)counters[0];  // written by stage 1, a previous launch
   for (;;) {
@@ -85,8 +92,8 @@ __global__ __launch_bounds__(64) void resolve_fast_kernel(const lt::DevScene* __
     if (base >= n) break;
     const int64_t k = base + lane;
     const bool live = k < n;
-    lt::analyze_fast<MAXY, RMAX, true, double>(*S, P, in, out, xtab, live ? defer[k] : 0, live,
-                                               lane, L);
+    lt::analyze_fast<MAXY, RMAX, true, VT>(*S, P, in, out, xtab, live ? defer[k] : 0, live, lane,
+                                           L);
   }
 }
 
@@ -104,15 +111,15 @@ __global__ __launch_bounds__(kBlock) void build_xtable_kernel(lt::lsq_xf* __rest
   xtab[idx] = f;
 }
 
-// waves of resolve_fast_kernel<MAXY, RMAX> the device holds at once
-template <int MAXY, int RMAX>
+// waves of resolve_fast_kernel<MAXY, RMAX, VT> the device holds at once
+template <int MAXY, int RMAX, class VT>
 static unsigned resolve_grid(int device) {
   static int cached_dev = -1;
   static unsigned cached = 0;
   if (cached_dev != device) {
     int per_cu = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, resolve_fast_kernel<MAXY, RMAX>, 64,
-                                                     0) != hipSuccess || per_cu < 1)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, resolve_fast_kernel<MAXY, RMAX, VT>,
+                                                     64, 0) != hipSuccess || per_cu < 1)
       per_cu = 1;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
         cus < 1)
@@ -327,13 +334,14 @@ int lt_analyze_tile(lt_ctx* c, const lt_scene* sc, const lt_params* prm, const l
   if (c->defer_cap < in->n_pix) {
     if (c->d_defer) HIP_OR_FAIL(c, hipFree(c->d_defer));
     c->d_defer = nullptr;
-    HIP_OR_FAIL(c, hipMalloc((void**)&c->d_defer, sizeof(int64_t) * (size_t)in->n_pix));
+    HIP_OR_FAIL(c, hipMalloc((void**)&c->d_defer, 2 * sizeof(int64_t) * (size_t)in->n_pix));
     if (!c->d_ndefer)
-      HIP_OR_FAIL(c, hipMalloc((void**)&c->d_ndefer, 2 * sizeof(unsigned long long)));
+      HIP_OR_FAIL(c, hipMalloc((void**)&c->d_ndefer, 4 * sizeof(unsigned long long)));
     c->defer_cap = in->n_pix;
   }
-  // [0]: deferred-pixel count (stage 1), [1]: the resolve stage's work counter
-  HIP_OR_FAIL(c, hipMemsetAsync(c->d_ndefer, 0, 2 * sizeof(unsigned long long), stream));
+  // [0]/[2]: deferred-pixel counts of the binary32 / binary64 lists (stage 1), [1]/[3]: the
+  // resolve launches' work counters
+  HIP_OR_FAIL(c, hipMemsetAsync(c->d_ndefer, 0, 4 * sizeof(unsigned long long), stream));
 
   EventPair* ep[2] = {nullptr, nullptr};
   if (c->timing) {
@@ -365,12 +373,17 @@ int lt_analyze_tile(lt_ctx* c, const lt_scene* sc, const lt_params* prm, const l
   HIP_OR_FAIL(c, hipGetLastError());
   if (ep[0]) HIP_OR_FAIL(c, hipEventRecord(ep[0]->stop, stream));
   if (ep[1]) HIP_OR_FAIL(c, hipEventRecord(ep[1]->start, stream));
+#define LT_LAUNCH_RESOLVE1(MY, RM, VT, LIST, CNT)                                            \
+  do {                                                                                      \
+    const unsigned g = resolve_grid<MY, RM, VT>(c->device);                                 \
+    dim3 rg((unsigned)(nwave < (int64_t)g ? nwave : (int64_t)g));                           \
+    hipLaunchKernelGGL((resolve_fast_kernel<MY, RM, VT>), rg, fblock, 0, stream, c->d_scene, \
+                       *prm, *in, *out, c->d_xtab, LIST, CNT);                              \
+  } while (0)
 #define LT_LAUNCH_RESOLVE(MY, RM)                                                            \
   do {                                                                                      \
-    const unsigned g = resolve_grid<MY, RM>(c->device);                                     \
-    dim3 rg((unsigned)(nwave < (int64_t)g ? nwave : (int64_t)g));                           \
-    hipLaunchKernelGGL((resolve_fast_kernel<MY, RM>), rg, fblock, 0, stream, c->d_scene,    \
-                       *prm, *in, *out, c->d_xtab, c->d_defer, c->d_ndefer);                \
+    LT_LAUNCH_RESOLVE1(MY, RM, float, c->d_defer, c->d_ndefer);                             \
+    LT_LAUNCH_RESOLVE1(MY, RM, double, c->d_defer + in->n_pix, c->d_ndefer + 2);            \
   } while (0)
   if (Y <= 32) {
     if (one) LT_LAUNCH_RESOLVE(32, 1); else if (few) LT_LAUNCH_RESOLVE(32, 4); else LT_LAUNCH_RESOLVE(32, 16);
@@ -380,6 +393,7 @@ int lt_analyze_tile(lt_ctx* c, const lt_scene* sc, const lt_params* prm, const l
     if (one) LT_LAUNCH_RESOLVE(64, 1); else if (few) LT_LAUNCH_RESOLVE(64, 4); else LT_LAUNCH_RESOLVE(64, 16);
   }
 #undef LT_LAUNCH_RESOLVE
+#undef LT_LAUNCH_RESOLVE1
   HIP_OR_FAIL(c, hipGetLastError());
   if (ep[1]) HIP_OR_FAIL(c, hipEventRecord(ep[1]->stop, stream));
   c->launches++;
@@ -391,9 +405,9 @@ int lt_ctx_last_deferred(lt_ctx* c, int64_t* n_deferred) {
   *n_deferred = 0;
   if (!c->d_ndefer) return LT_OK;
   HIP_OR_FAIL(c, hipSetDevice(c->device));
-  unsigned long long v = 0;
-  HIP_OR_FAIL(c, hipMemcpy(&v, c->d_ndefer, sizeof v, hipMemcpyDeviceToHost));
-  *n_deferred = (int64_t)v;
+  unsigned long long v[4] = {0, 0, 0, 0};
+  HIP_OR_FAIL(c, hipMemcpy(v, c->d_ndefer, sizeof v, hipMemcpyDeviceToHost));
+  *n_deferred = (int64_t)(v[0] + v[2]);
   return LT_OK;
 }
 

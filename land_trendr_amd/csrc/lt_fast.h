@@ -62,12 +62,14 @@ struct WaveLds {
   int32_t year[LT_MAX_YEARS];  // the scene's calendar year per slot (64 words: one bank each)
 };
 
-// EXACT = false (analyze stage): the lazy DP; returns false when the pixel's optimal path crosses
-// an ambiguous DP column (or its values are not exact in binary32) — the resolve stage redoes it.
+// EXACT = false (analyze stage): the lazy DP; returns kDeferExact when the pixel's optimal path
+// crosses an ambiguous DP column, kDeferWide when its values are not exact in binary32 (the
+// resolve stage redoes them with binary32 / binary64 LDS series), else kDone.
 // EXACT = true (resolve stage): the exact-OPT DP, every column decided with the emulated LAPACK
-// residual of each start inside the error window; always returns true.
+// residual of each start inside the error window; always kDone.
+enum { kDone = 0, kDeferExact = 1, kDeferWide = 2 };
 template <int MAXY, int RMAX, bool EXACT, class VT>
-__device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const lt_tile_in& in,
+__device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const lt_tile_in& in,
                                    const lt_tile_out& out, const lsq_xf* __restrict__ xtab,
                                    int64_t p, bool live, int lane, WaveLds<MAXY, VT>& L) {
   const int Y = S.n_years;
@@ -139,7 +141,7 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
         const double v = val[u];
         if (T == 0) y0 = S.year[y];
         const VT vs = (VT)v;
-        if constexpr (!EXACT) {
+        if constexpr (!EXACT || sizeof(VT) == 4) {
           if (!((double)vs == v)) f32_bad = true;
         }
         L.ys[T][lane] = vs;
@@ -573,7 +575,14 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
     for (int r = 0; r < RMAX; r++)
       if (r < P.n_rules) rs[r].write(P.rules[r], out, (int64_t)r * os + p);
   }
-  if (!live || deferred) return !deferred;
+  if (!live || deferred) {
+    if (!deferred) return kDone;
+    if constexpr (EXACT) {  // a binary32 resolve given a value binary32 cannot hold: unreachable
+      if (out.status) out.status[p] = status | LT_ST_NUMERIC;
+      return kDone;
+    }
+    return f32_bad ? kDeferWide : kDeferExact;
+  }
   if (!ok) {  // the reference raises for this pixel: per-year fields of present years are NaN
     for (uint64_t m = pres; m; m &= m - 1) {
       const int64_t o = (int64_t)__builtin_ctzll(m) * os + p;
@@ -588,7 +597,7 @@ __device__ inline bool analyze_fast(const DevScene& S, const lt_params& P, const
   }
   if (out.n_years) out.n_years[p] = T;
   if (out.status) out.status[p] = status;
-  return true;
+  return kDone;
 }
 
 }  // namespace lt
