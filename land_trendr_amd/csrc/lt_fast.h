@@ -170,31 +170,32 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
   uint64_t spike = 0;
   int n = 0;
   if (Tmax >= 2) {
-    const int n8 = ok ? T - (T % 8) : 0;
-    // np.sum: 8 accumulators over the first n - n%8 elements (n >= 8), else sequential
+    // np.sum: n >= 8: eight accumulators over the first n - n%8 elements
+    // (r_k starts as element k), their tree, then the rest sequentially; n < 8: sequential.
+    // Two uniform loops: the accumulator block up to the wave's largest n8, the sequential tail
+    // from the wave's smallest n8 (per-lane predicates select which elements a lane takes).
+    const int n8 = (ok && T >= 8) ? T - (T % 8) : 0;
+    const int n8max = wave_max(n8);
+    const int n8min = -wave_max(-n8);
     auto npsum = [&](auto term) {
       double r0 = 0.0, r1 = 0.0, r2 = 0.0, r3 = 0.0, r4 = 0.0, r5 = 0.0, r6 = 0.0, r7 = 0.0;
-      double seq = 0.0;
-      for (int t = 0; t < Tmax; t++) {
-        if (!(ok && t < T)) continue;
-        const double a = term(t);
-        if (T < 8) {
-          seq += a;
-        } else if (t < n8) {
-          switch (t & 7) {
-            case 0: r0 = t < 8 ? a : r0 + a; break;
-            case 1: r1 = t < 8 ? a : r1 + a; break;
-            case 2: r2 = t < 8 ? a : r2 + a; break;
-            case 3: r3 = t < 8 ? a : r3 + a; break;
-            case 4: r4 = t < 8 ? a : r4 + a; break;
-            case 5: r5 = t < 8 ? a : r5 + a; break;
-            case 6: r6 = t < 8 ? a : r6 + a; break;
-            default: r7 = t < 8 ? a : r7 + a; break;
-          }
-          if (t == n8 - 1) seq = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
-        } else {
-          seq += a;
+      for (int t = 0; t < n8max; t++) {
+        const bool in = t < n8;
+        const double a = in ? term(t) : 0.0;
+        switch (t & 7) {  // wave-uniform
+          case 0: r0 = !in ? r0 : t < 8 ? a : r0 + a; break;
+          case 1: r1 = !in ? r1 : t < 8 ? a : r1 + a; break;
+          case 2: r2 = !in ? r2 : t < 8 ? a : r2 + a; break;
+          case 3: r3 = !in ? r3 : t < 8 ? a : r3 + a; break;
+          case 4: r4 = !in ? r4 : t < 8 ? a : r4 + a; break;
+          case 5: r5 = !in ? r5 : t < 8 ? a : r5 + a; break;
+          case 6: r6 = !in ? r6 : t < 8 ? a : r6 + a; break;
+          default: r7 = !in ? r7 : t < 8 ? a : r7 + a; break;
         }
+      }
+      double seq = n8 > 0 ? ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)) : 0.0;
+      for (int t = n8min; t < Tmax; t++) {
+        if (ok && t >= n8 && t < T) seq += term(t);
       }
       return seq;
     };
@@ -204,29 +205,36 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
                                        return d * d;
                                      }) /
                                      (double)T);
+    // the 3-window scan (on the original series) fused with dropna's in-place compaction: point
+    // t is written to slot n <= t once its spike decision is known; ys[t + 1] is read first
+    uint64_t rem = pres;
     double last_good = ok ? L.ys[0][lane] : 0.0;
     double xv = last_good, yv = ok ? L.ys[1][lane] : 0.0;
-    for (int t = 1; t + 1 < Tmax; t++) {
-      if (!(ok && t + 1 < T)) continue;
-      const double zv = L.ys[t + 1][lane];
-      const bool mono = (xv <= yv && yv <= zv) || (xv >= yv && yv >= zv);
-      if (!mono && (__builtin_fabs(yv - xv) > sd && __builtin_fabs(yv - zv) > sd) &&
-          yv != last_good) {
-        spike |= 1ull << t;
-      } else {
-        last_good = yv;
-      }
-      xv = yv;
-      yv = zv;
-    }
-    // dropna: compact the non-spike points in place (k <= t)
-    uint64_t rem = pres;
-    for (int t = 0; t < Tmax; t++) {
-      if (!(ok && t < T)) continue;
+    if (ok) {  // point 0 is never a spike
       const int y = __builtin_ctzll(rem);
       rem &= rem - 1;
-      if ((spike >> t) & 1) continue;
-      L.ys[n][lane] = L.ys[t][lane];
+      L.xn[0][lane] = (uint8_t)(L.year[y] - y0);
+      n = 1;
+    }
+    for (int t = 1; t < Tmax; t++) {
+      if (!(ok && t < T)) continue;
+      bool is_spike = false;
+      if (t + 1 < T) {  // the last point is never a spike
+        const double zv = L.ys[t + 1][lane];
+        const bool mono = (xv <= yv && yv <= zv) || (xv >= yv && yv >= zv);
+        is_spike = !mono && (__builtin_fabs(yv - xv) > sd && __builtin_fabs(yv - zv) > sd) &&
+                   yv != last_good;
+        if (!is_spike) last_good = yv;
+        xv = yv;
+        yv = zv;
+      }
+      const int y = __builtin_ctzll(rem);
+      rem &= rem - 1;
+      if (is_spike) {
+        spike |= 1ull << t;
+        continue;
+      }
+      if (n != t) L.ys[n][lane] = L.ys[t][lane];
       L.xn[n][lane] = (uint8_t)(L.year[y] - y0);
       n++;
     }
