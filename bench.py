@@ -158,7 +158,9 @@ def main():
     eng = get_engine(local)
     if bands_in:
         index_fn = eng.compile_index(IndexProgram('B1 - B2', band_dtype='int16'))
-        index_buf = torch.empty((meta.n_obs, args.tile), dtype=torch.int16, device=dev)
+        # the index raster of the whole scene ([K, P], like rast_algebra's per-scene output):
+        # tile views share the row stride of the cloud-mask planes (one stride per tile input)
+        index_buf = torch.empty((meta.n_obs, P), dtype=torch.int16, device=dev)
     idx_events = []
     fields = ['status', 'matched', 'class_val', 'onset_year', 'duration', 'magnitude']
     if cfg['trendline']:
@@ -185,7 +187,7 @@ def main():
                         enable_timing=True)
                     e0.record()
                 values = eng.index_tile(index_fn, sc.bands[:, :, p0:p1],
-                                        out=index_buf[:, :p1 - p0])
+                                        out=index_buf[:, p0:p1])
                 if timed:
                     e1.record()
                     idx_events.append((e0, e1))

@@ -245,95 +245,182 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
   bool deferred = live && T >= 2 && f32_bad;
   uint64_t vmask = 0;  // vertices over non-spike indices
   if constexpr (EXACT) {
-    // ---- exact-OPT DP: closed-form intervals, then the emulated LAPACK residual for every
-    // start whose interval reaches the column's smallest upper bound; first exact minimum ----
-    const double c = P.line_cost;
-    const double inf = __builtin_inf();
-    double OPT[MAXY + 1];
-#pragma unroll
-    for (int k = 0; k <= MAXY; k++) OPT[k] = 0.0;
-    double SyyAll = 0.0;  // sum of y^2 over the points 0..j (early-exit bound, as below)
-    const bool prune = c >= 0.0;
-    for (int jj = 0; jj < nmax; jj++) {
-      const int j = __builtin_amdgcn_readfirstlane(jj);
-      const bool col = j < n;
-      double Sy = 0.0, Sxy = 0.0, Syy = 0.0;
-      int Sx = 0, Sxx = 0;
-      double H = inf;
-      // starts whose interval reaches the smallest upper end seen so far (itself included): a
-      // superset of those reaching the final one, where the exact minimum lies
-      uint64_t cand = 0;
-      {
-        const double yj = (double)L.ys[j][lane];
-        SyyAll = __builtin_fma(yj, yj, SyyAll);
-      }
-#pragma unroll
-      for (int i = MAXY - 1; i >= 0; i--) {
-        if (i > j) continue;  // wave-uniform
-        const int xi = L.xn[i][lane];
-        const double yi = (double)L.ys[i][lane];
-        Sx += xi;
-        Sxx += xi * xi;
-        Sy += yi;
-        Sxy = __builtin_fma((double)xi, yi, Sxy);
-        Syy = __builtin_fma(yi, yi, Syy);
-        const int m = j - i + 1;
-        double e = 0.0, w = 0.0;  // m <= 2: exact residual 0 on an exact OPT: v is the reference
-        if (m >= 3) {
-          const double md = (double)m;
-          const double D = (double)(m * Sxx - Sx * Sx);
-          const double t1 = __builtin_fma(md, Syy, -(Sy * Sy));
-          const double N1 = __builtin_fma(md, Sxy, -((double)Sx * Sy));
-          const double den = md * D;
-          double r = __builtin_amdgcn_rcp(den);
-          r = __builtin_fma(r, __builtin_fma(-den, r, 1.0), r);
-          e = __builtin_fma(t1, D, -(N1 * N1)) * r;
-          e = e < 0.0 ? 0.0 : e;
+    if constexpr (MAXY <= 32) {
+      // ---- exact-OPT DP: closed-form intervals, then the emulated LAPACK residual for every
+      // start whose interval reaches the column's smallest upper bound; first exact minimum ----
+      const double c = P.line_cost;
+      const double inf = __builtin_inf();
+      // OPT lives in per-lane private memory (read at wave-uniform and per-lane indices)
+      double OPT[MAXY + 1];
+      OPT[0] = 0.0;
+      double SyyAll = 0.0;  // sum of y^2 over the points 0..j (early-exit bound, as below)
+      const bool prune = c >= 0.0;
+      for (int jj = 0; jj < nmax; jj++) {
+        const int j = __builtin_amdgcn_readfirstlane(jj);
+        const bool col = j < n;
+        double Sy = 0.0, Sxy = 0.0, Syy = 0.0;
+        int Sx = 0, Sxx = 0;
+        double H = inf;
+        // starts whose interval reaches the smallest upper end seen so far (itself included): a
+        // superset of those reaching the final one, where the exact minimum lies
+        uint64_t cand = 0;
+        {
+          const double yj = (double)L.ys[j][lane];
+          SyyAll = __builtin_fma(yj, yj, SyyAll);
         }
-        const double v = (e + c) + OPT[i];
-        if (m >= 3) w = __builtin_fma(0x1p-50, __builtin_fabs(v), kScreen * Syy);
-        if (v - w <= H) cand |= 1ull << i;
-        H = v + w < H ? v + w : H;
-        // early exit (dp_start_bound): no start below i can reach H
-        if (prune && m >= 3 && !__ballot(col && !(dp_start_bound(e, OPT[i], 0.0, c, SyyAll) > H)))
-          break;
-      }
-      const int nc = col ? __builtin_popcountll(cand) : 0;
-      const int ncmax = wave_max(nc);
-      double best = inf;
-      int bi = 0;
-      for (int r = 0; r < ncmax; r++) {  // candidates in increasing start order, lockstep
-        const bool act = r < nc;
-        const int i = act ? __builtin_ctzll(cand) : 0;
-        if (act) cand &= cand - 1;
-        const int m = j - i + 1;
-        const bool ls = act && m >= 3;
-        double e = 0.0;
-        if (__ballot(ls)) {
-          double sm, sb, ssr;
-          const int rc = lsq_lockstep(
-              ls, m, [&](int k) { return (int)L.xn[i + k][lane]; },
-              [&](int k) { return (double)L.ys[i + k][lane]; }, xtab, false, true, sm, sb, ssr);
-          if (ls) {
-            if (rc < 0) status |= LT_ST_NUMERIC;
-            e = ssr;
+        for (int ii = j; ii >= 0; ii--) {
+          const int i = __builtin_amdgcn_readfirstlane(ii);  // wave-uniform start
+          const int xi = L.xn[i][lane];
+          const double yi = (double)L.ys[i][lane];
+          Sx += xi;
+          Sxx += xi * xi;
+          Sy += yi;
+          Sxy = __builtin_fma((double)xi, yi, Sxy);
+          Syy = __builtin_fma(yi, yi, Syy);
+          const int m = j - i + 1;
+          double e = 0.0, w = 0.0;  // m <= 2: exact residual 0 on an exact OPT: v is the reference
+          if (m >= 3) {
+            const double md = (double)m;
+            const double D = (double)(m * Sxx - Sx * Sx);
+            const double t1 = __builtin_fma(md, Syy, -(Sy * Sy));
+            const double N1 = __builtin_fma(md, Sxy, -((double)Sx * Sy));
+            const double den = md * D;
+            double r = __builtin_amdgcn_rcp(den);
+            r = __builtin_fma(r, __builtin_fma(-den, r, 1.0), r);
+            e = __builtin_fma(t1, D, -(N1 * N1)) * r;
+            e = e < 0.0 ? 0.0 : e;
+          }
+          const double v = (e + c) + OPT[i];
+          if (m >= 3) w = __builtin_fma(0x1p-50, __builtin_fabs(v), kScreen * Syy);
+          if (v - w <= H) cand |= 1ull << i;
+          H = v + w < H ? v + w : H;
+          // early exit (dp_start_bound): no start below i can reach H
+          if (prune && m >= 3 && !__ballot(col && !(dp_start_bound(e, OPT[i], 0.0, c, SyyAll) > H)))
+            break;
+        }
+        const int nc = col ? __builtin_popcountll(cand) : 0;
+        const int ncmax = wave_max(nc);
+        double best = inf;
+        int bi = 0;
+        for (int r = 0; r < ncmax; r++) {  // candidates in increasing start order, lockstep
+          const bool act = r < nc;
+          const int i = act ? __builtin_ctzll(cand) : 0;
+          if (act) cand &= cand - 1;
+          const int m = j - i + 1;
+          const bool ls = act && m >= 3;
+          double e = 0.0;
+          if (__ballot(ls)) {
+            double sm, sb, ssr;
+            const int rc = lsq_lockstep(
+                ls, m, [&](int k) { return (int)L.xn[i + k][lane]; },
+                [&](int k) { return (double)L.ys[i + k][lane]; }, xtab, false, true, sm, sb, ssr);
+            if (ls) {
+              if (rc < 0) status |= LT_ST_NUMERIC;
+              e = ssr;
+            }
+          }
+          const double v = (e + c) + OPT[i];  // per-lane index
+          if (act && v < best) {  // increasing start order + strict "<": the first minimum
+            best = v;
+            bi = i;
           }
         }
-        double o = 0.0;
-#pragma unroll
-        for (int k = 0; k < MAXY; k++)
-          if (k == i) o = OPT[k];  // per-lane index: select chain
-        const double v = (e + c) + o;
-        if (act && v < best) {  // increasing start order + strict "<": the first minimum
-          best = v;
-          bi = i;
+        if (col) {
+          L.ag[j][lane] = (uint8_t)bi;
+          OPT[j + 1] = best;
         }
       }
-      if (col) {
-        L.ag[j][lane] = (uint8_t)bi;
+    } else {  // larger series: OPT in registers (private memory would thrash L1)
+      // ---- exact-OPT DP: closed-form intervals, then the emulated LAPACK residual for every
+      // start whose interval reaches the column's smallest upper bound; first exact minimum ----
+      const double c = P.line_cost;
+      const double inf = __builtin_inf();
+      double OPT[MAXY + 1];
 #pragma unroll
-        for (int k = 1; k <= MAXY; k++)
-          if (k == j + 1) OPT[k] = best;  // wave-uniform index
+      for (int k = 0; k <= MAXY; k++) OPT[k] = 0.0;
+      double SyyAll = 0.0;  // sum of y^2 over the points 0..j (early-exit bound, as below)
+      const bool prune = c >= 0.0;
+      for (int jj = 0; jj < nmax; jj++) {
+        const int j = __builtin_amdgcn_readfirstlane(jj);
+        const bool col = j < n;
+        double Sy = 0.0, Sxy = 0.0, Syy = 0.0;
+        int Sx = 0, Sxx = 0;
+        double H = inf;
+        // starts whose interval reaches the smallest upper end seen so far (itself included): a
+        // superset of those reaching the final one, where the exact minimum lies
+        uint64_t cand = 0;
+        {
+          const double yj = (double)L.ys[j][lane];
+          SyyAll = __builtin_fma(yj, yj, SyyAll);
+        }
+#pragma unroll
+        for (int i = MAXY - 1; i >= 0; i--) {
+          if (i > j) continue;  // wave-uniform
+          const int xi = L.xn[i][lane];
+          const double yi = (double)L.ys[i][lane];
+          Sx += xi;
+          Sxx += xi * xi;
+          Sy += yi;
+          Sxy = __builtin_fma((double)xi, yi, Sxy);
+          Syy = __builtin_fma(yi, yi, Syy);
+          const int m = j - i + 1;
+          double e = 0.0, w = 0.0;  // m <= 2: exact residual 0 on an exact OPT: v is the reference
+          if (m >= 3) {
+            const double md = (double)m;
+            const double D = (double)(m * Sxx - Sx * Sx);
+            const double t1 = __builtin_fma(md, Syy, -(Sy * Sy));
+            const double N1 = __builtin_fma(md, Sxy, -((double)Sx * Sy));
+            const double den = md * D;
+            double r = __builtin_amdgcn_rcp(den);
+            r = __builtin_fma(r, __builtin_fma(-den, r, 1.0), r);
+            e = __builtin_fma(t1, D, -(N1 * N1)) * r;
+            e = e < 0.0 ? 0.0 : e;
+          }
+          const double v = (e + c) + OPT[i];
+          if (m >= 3) w = __builtin_fma(0x1p-50, __builtin_fabs(v), kScreen * Syy);
+          if (v - w <= H) cand |= 1ull << i;
+          H = v + w < H ? v + w : H;
+          // early exit (dp_start_bound): no start below i can reach H
+          if (prune && m >= 3 && !__ballot(col && !(dp_start_bound(e, OPT[i], 0.0, c, SyyAll) > H)))
+            break;
+        }
+        const int nc = col ? __builtin_popcountll(cand) : 0;
+        const int ncmax = wave_max(nc);
+        double best = inf;
+        int bi = 0;
+        for (int r = 0; r < ncmax; r++) {  // candidates in increasing start order, lockstep
+          const bool act = r < nc;
+          const int i = act ? __builtin_ctzll(cand) : 0;
+          if (act) cand &= cand - 1;
+          const int m = j - i + 1;
+          const bool ls = act && m >= 3;
+          double e = 0.0;
+          if (__ballot(ls)) {
+            double sm, sb, ssr;
+            const int rc = lsq_lockstep(
+                ls, m, [&](int k) { return (int)L.xn[i + k][lane]; },
+                [&](int k) { return (double)L.ys[i + k][lane]; }, xtab, false, true, sm, sb, ssr);
+            if (ls) {
+              if (rc < 0) status |= LT_ST_NUMERIC;
+              e = ssr;
+            }
+          }
+          double o = 0.0;
+#pragma unroll
+          for (int k = 0; k < MAXY; k++)
+            if (k == i) o = OPT[k];  // per-lane index: select chain
+          const double v = (e + c) + o;
+          if (act && v < best) {  // increasing start order + strict "<": the first minimum
+            best = v;
+            bi = i;
+          }
+        }
+        if (col) {
+          L.ag[j][lane] = (uint8_t)bi;
+#pragma unroll
+          for (int k = 1; k <= MAXY; k++)
+            if (k == j + 1) OPT[k] = best;  // wave-uniform index
+        }
       }
     }
     if (n >= 1) {
@@ -347,9 +434,8 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
   } else if (nmax >= 1 && LT_ABLATE != 2) {
     const double c = P.line_cost;
     const double inf = __builtin_inf();
-    double OPTa[MAXY + 1];
-#pragma unroll
-    for (int k = 0; k <= MAXY; k++) OPTa[k] = 0.0;
+    double OPTa[MAXY + 1];  // per-lane private memory (wave-uniform indices)
+    OPTa[0] = 0.0;
     uint64_t exact = 1;      // bit k: OPTa[k] is the reference value itself
     double Emax = 0.0;       // bound on |OPTa[k] - OPT[k]| for every inexact k so far
     double opt_j = 0.0, opt_jm1 = 0.0;  // OPTa[j] and OPTa[j-1] (the 1- and 2-point starts)
@@ -397,9 +483,8 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
         const double yj = (double)L.ys[j][lane];
         SyyAll = __builtin_fma(yj, yj, SyyAll);
       }
-#pragma unroll
-      for (int i = MAXY - 1; i >= 0; i--) {
-        if (i > j) continue;  // wave-uniform
+      for (int ii = j; ii >= 0; ii--) {
+        const int i = __builtin_amdgcn_readfirstlane(ii);  // wave-uniform start
         const int xi = L.xn[i][lane];
         const double yi = (double)L.ys[i][lane];
         Sx += xi;
@@ -462,9 +547,7 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
       }
       if (col) {
         L.ag[j][lane] = (uint8_t)a;
-#pragma unroll
-        for (int k = 1; k <= MAXY; k++)
-          if (k == j + 1) OPTa[k] = vnew;  // wave-uniform index
+        OPTa[j + 1] = vnew;  // wave-uniform index
         if (exnew) exact |= 2ull << j;
         Emax = enew > Emax ? enew : Emax;
         opt_jm1 = opt_j;
