@@ -59,6 +59,31 @@ class GeoTiff:
         self.tiepoint = t.get(33922)
         self.geokeys = t.get(34735)
 
+    def geotransform(self):
+        """GDAL's GetGeoTransform() of this file: (top_left_x, pix_width, x_rot, top_left_y,
+        y_rot, pix_height), from ModelTransformation (34264) or ModelTiepoint + ModelPixelScale,
+        as GDAL's GTiff driver derives it (PixelIsPoint rasters shifted by half a pixel, the
+        driver's default). No georeferencing: GDAL's default (0, 1, 0, 0, 0, 1)."""
+        point = False
+        if self.geokeys:  # GTRasterTypeGeoKey (1025) == RasterPixelIsPoint (2)
+            g = self.geokeys
+            for k in range(4, 4 + 4 * int(g[3]), 4):
+                if g[k] == 1025 and g[k + 1] == 0 and g[k + 3] == 2:
+                    point = True
+        mt = self.tags.get(34264)
+        if mt is not None:
+            gt = [mt[3], mt[0], mt[1], mt[7], mt[4], mt[5]]
+        elif self.tiepoint and self.pixel_scale:
+            i, j, _, x, y, _ = self.tiepoint[:6]
+            sx, sy = self.pixel_scale[0], self.pixel_scale[1]
+            gt = [x - i * sx, sx, 0.0, y + j * sy, 0.0, -sy]
+        else:
+            return (0.0, 1.0, 0.0, 0.0, 0.0, 1.0)
+        if point:
+            gt[0] -= gt[1] * 0.5 + gt[2] * 0.5
+            gt[3] -= gt[4] * 0.5 + gt[5] * 0.5
+        return tuple(float(v) for v in gt)
+
     def _ifd(self, off):
         d, bo = self._d, self._bo
         (n,) = struct.unpack(bo + 'H', d[off:off + 2])

@@ -1,0 +1,264 @@
+"""Input ingest: the mapper side of the reference pipeline, restated
+without GDAL/OGR/S3 over co-registered GeoTIFF stacks.
+
+Reference flow, per analysis raster (MRLandTrendrJob.parse_mapper, mr_land_trendr_job.py:48-81):
+  rast_dl -> rast_algebra(index_eqn) -> filename2date -> apply_grid(index raster, grid, mask)
+  -> one (pix_ctr_wkt, {'val', 'date'}) pair per grid point whose mask value is not 0.
+The reducer then sees, per grid point, the list of its observations.
+
+Here the same data is assembled as planes for the GPU: `ingest_stack` gathers, for every raster k
+and grid point p, the band samples bands[k, :, p] and valid[k, p] (1 unless the point is off the
+raster or its cloud mask value is 0, exactly the cases apply_grid skips), and the index equation
+runs on the GPU over those samples (utils.index_tile — elementwise, so evaluating it at the grid
+points equals sampling the evaluated raster). The per-point generators (`serialize_rast`,
+`apply_grid`) are kept with the reference's semantics, including its WKT text (Python 2 float
+formatting), numpy's negative-index wrap in pt2val and the exceptions it swallows.
+"""
+import datetime as _dt
+import glob
+import os
+import shutil
+import tarfile
+import zipfile
+
+import numpy as np
+
+from .geotiff import GeoTiff
+
+RAST_TRIGGER = 'ledaps'      # settings.py:11
+MASK_TRIGGER = 'cloudmask'   # settings.py:12
+
+
+# ---- string parsing (utils.py:189-225) ---------------------------------------------------------
+def filename2date(fn):
+    """utils.filename2date (utils.py:204-217): 'LE7045029_1999_211_..._cloudmask.tif.tar.gz'
+    -> '1999-07-30' (year, day of year from the 2nd and 3rd '_' fields)."""
+    chunks = os.path.basename(fn).split('_')
+    yr, days = int(chunks[1]), int(chunks[2])
+    d = _dt.datetime(year=yr, month=1, day=1) + _dt.timedelta(days=days - 1)
+    return d.strftime('%Y-%m-%d')
+
+
+def py2_float_str(x):
+    """Python 2's str(float): repr with 12 significant digits ('%.12g'), '.0' appended when the
+    text would read as an integer (what '%s' % x gives in the reference's WKT, utils.py:321)."""
+    x = float(x)
+    if x != x:
+        return 'nan'
+    if x in (float('inf'), float('-inf')):
+        return 'inf' if x > 0 else '-inf'
+    s = '%.12g' % x
+    if not any(ch in s for ch in '.en'):
+        s += '.0'
+    return s
+
+
+def point_wkt(x, y):
+    return 'POINT(%s %s)' % (py2_float_str(x), py2_float_str(y))
+
+
+def parse_point_wkt(wkt):
+    """OGR's CreateGeometryFromWkt(...).GetX()/GetY() for 'POINT(x y)' (and data2raster's own
+    split, utils.py:430-431): correctly rounded decimal -> binary64, as float()."""
+    clean = wkt.replace('POINT', '').replace('(', '').replace(')', '').strip()
+    a, b = clean.split()
+    return float(a), float(b)
+
+
+# ---- compression (utils.py:11-45) --------------------------------------------------------------
+def decompress(filename, out_dir='/tmp/decompressed'):
+    """utils.decompress: extract a zip or tar(.gz) into out_dir and list its files; an existing
+    out_dir is returned as is (the reference's cache); ValueError for any other file type."""
+    if os.path.exists(out_dir):
+        return glob.glob(os.path.join(out_dir, '*'))
+    os.makedirs(out_dir)
+    ok = False
+    try:
+        if zipfile.is_zipfile(filename):
+            zipfile.ZipFile(filename, 'r').extractall(out_dir)
+        elif tarfile.is_tarfile(filename):
+            with tarfile.open(filename, 'r') as tf:
+                tf.extractall(out_dir, filter='data')
+        else:
+            raise ValueError('Invalid file type - must be tar.gz or zip')
+        ok = True
+    finally:
+        if not ok:
+            shutil.rmtree(out_dir)
+    return [os.path.join(out_dir, f) for f in os.listdir(out_dir)]
+
+
+def rast_local(fn, work_dir):
+    """rast_dl (utils.py:126-135) minus the download: a compressed raster is decompressed into
+    work_dir/<name without .tif/.tar.gz/.zip> and its first file returned; a plain .tif as is."""
+    if zipfile.is_zipfile(fn) or (os.path.isfile(fn) and tarfile.is_tarfile(fn)):
+        name = os.path.basename(fn).replace('.tif', '').replace('.tar.gz', '').replace('.zip', '')
+        return sorted(decompress(fn, os.path.join(work_dir, name)))[0]
+    return fn
+
+
+# ---- grid (utils.py:252-370) -------------------------------------------------------------------
+def _open(r):
+    return r if isinstance(r, GeoTiff) else GeoTiff(r)
+
+
+def get_pix_offsets_for_point(gt, lng, lat):
+    """utils.get_pix_offsets_for_point (utils.py:252-269) on a geotransform tuple: int() of the
+    distance over the pixel size, i.e. truncation toward zero."""
+    top_left_x, pix_width, _, top_left_y, _, pix_height = gt
+    x_offset = int((lng - top_left_x) * 1.0 / pix_width)
+    y_offset = int((lat - top_left_y) * 1.0 / pix_height)
+    return x_offset, y_offset
+
+
+def pt2val(gt, pt_wkt, raster_array):
+    """utils.pt2val (utils.py:285-297): raster_array[y_off, x_off] with numpy's indexing rules
+    (negative offsets wrap, out-of-range ones raise IndexError)."""
+    lng, lat = parse_point_wkt(pt_wkt)
+    x_off, y_off = get_pix_offsets_for_point(gt, lng, lat)
+    return raster_array[y_off, x_off]
+
+
+def serialize_rast(rast_fn, extra_data={}):
+    """utils.serialize_rast (utils.py:300-325): (pixel-centre WKT, {'val': float, **extra}) for
+    every pixel of band 1, columns outer, rows inner."""
+    ds = _open(rast_fn)
+    top_left_x, pix_width, _, top_left_y, _, pix_height = ds.geotransform()
+    pixvals = ds.read()[0]
+    for xoff in range(ds.width):
+        x = top_left_x + (xoff + 0.5) * pix_width
+        for yoff in range(ds.height):
+            y = top_left_y + (yoff + 0.5) * pix_height
+            pt_data = {'val': float(pixvals[yoff, xoff])}
+            pt_data.update(extra_data)
+            yield point_wkt(x, y), pt_data
+
+
+def grid_wkts(ds):
+    """The WKT column rast2grid writes, vectorised (same operations, same order)."""
+    ds = _open(ds)
+    top_left_x, pix_width, _, top_left_y, _, pix_height = ds.geotransform()
+    xs = top_left_x + (np.arange(ds.width, dtype=np.float64) + 0.5) * pix_width
+    ys = top_left_y + (np.arange(ds.height, dtype=np.float64) + 0.5) * pix_height
+    xt = [py2_float_str(v) for v in xs]
+    yt = [py2_float_str(v) for v in ys]
+    return ['POINT(%s %s)' % (a, b) for a in xt for b in yt]
+
+
+def rast2grid(rast_fn, out_csv='/tmp/grid.csv'):
+    """utils.rast2grid (utils.py:361-370): CSV with a 'pix_ctr_wkt' column, one pixel centre per
+    line (pandas to_csv, index=False: no quoting is needed for 'POINT(x y)')."""
+    with open(out_csv, 'w') as f:
+        f.write('pix_ctr_wkt\n')
+        for w in grid_wkts(rast_fn):
+            f.write(w + '\n')
+    return out_csv
+
+
+def read_grid(grid):
+    """The 'pix_ctr_wkt' column of a grid CSV (or a list of WKTs, returned as is)."""
+    if not isinstance(grid, (str, os.PathLike)):
+        return list(grid)
+    with open(grid) as f:
+        header = f.readline().rstrip('\n').split(',')
+        col = header.index('pix_ctr_wkt')
+        return [line.rstrip('\n').split(',')[col].strip('"') for line in f if line.strip()]
+
+
+def grid_points(grid):
+    """Grid WKTs -> (lng, lat) float64 arrays."""
+    pts = np.array([parse_point_wkt(w) for w in read_grid(grid)], np.float64).reshape(-1, 2)
+    return pts[:, 0].copy(), pts[:, 1].copy()
+
+
+def grid_offsets(gt, shape, lng, lat):
+    """Vectorised pt2val addressing for many points: flat pixel index of each point in a raster
+    of `shape` and whether pt2val would return a value there (numpy wrap for offsets in
+    [-n, 0), IndexError -> False beyond)."""
+    rows, cols = shape
+    top_left_x, pix_width, _, top_left_y, _, pix_height = gt
+    xo = np.trunc((lng - top_left_x) * 1.0 / pix_width)
+    yo = np.trunc((lat - top_left_y) * 1.0 / pix_height)
+    ok = (xo >= -cols) & (xo < cols) & (yo >= -rows) & (yo < rows)
+    xo = np.where(ok, xo, 0).astype(np.int64)
+    yo = np.where(ok, yo, 0).astype(np.int64)
+    xo = np.where(xo < 0, xo + cols, xo)
+    yo = np.where(yo < 0, yo + rows, yo)
+    return yo * cols + xo, ok
+
+
+def mask_name(rast_fn):
+    """parse_mapper's mask key (mr_land_trendr_job.py:59): RAST_TRIGGER -> MASK_TRIGGER."""
+    return rast_fn.replace(RAST_TRIGGER, MASK_TRIGGER)
+
+
+def apply_grid(rast_fn, grid_fn, extra_data={}, mask_fn=None):
+    """utils.apply_grid (utils.py:328-359), per point: (wkt, {'val': float(v), **extra}) for the
+    grid points on the raster whose mask value (when the mask has one there) is not 0."""
+    ds = _open(rast_fn)
+    gt, arr = ds.geotransform(), ds.read()[0]
+    if mask_fn:
+        mds = _open(mask_fn)
+        mgt, marr = mds.geotransform(), mds.read()[0]
+    for wkt in read_grid(grid_fn):
+        try:
+            val = pt2val(gt, wkt, arr)
+        except Exception:  # grid points off the raster
+            continue
+        if mask_fn:
+            try:
+                if pt2val(mgt, wkt, marr) == 0:
+                    continue
+            except Exception:  # an invalid mask is ignored
+                pass
+        pt_data = {'val': float(val)}
+        pt_data.update(extra_data)
+        yield wkt, pt_data
+
+
+def analysis_rasters(paths):
+    """setup_mapper's raster list (mr_land_trendr_job.py:29-32): the files whose name holds
+    RAST_TRIGGER, in key order (S3 lists keys lexicographically)."""
+    return sorted(p for p in paths if RAST_TRIGGER in os.path.basename(p))
+
+
+def ingest_stack(rast_fns, grid, mask_fns=None, bands=None):
+    """parse_mapper over every analysis raster, as planes for analysis_reducer_batch.
+
+    rast_fns: the (decompressed) analysis rasters, in the mapper order that becomes each pixel's
+    observation order; grid: CSV path or WKT list (P points); mask_fns: per raster the mask path
+    or None (default: mask_name(fn) when that file exists); bands: the band numbers to gather
+    (default: all bands of each raster).
+    Returns dict(dates=['YYYY-MM-DD'] * K, bands=[K, nb, P] in the rasters' sample type,
+    band_numbers=[nb], valid=[K, P] uint8)."""
+    lng, lat = grid_points(grid)
+    P = len(lng)
+    K = len(rast_fns)
+    if mask_fns is None:
+        mask_fns = [mask_name(f) if os.path.exists(mask_name(f)) and mask_name(f) != f else None
+                    for f in rast_fns]
+    out_bands, valid, dates, dtype, numbers = None, np.zeros((K, P), np.uint8), [], None, None
+    for k, fn in enumerate(rast_fns):
+        ds = _open(fn)
+        a = ds.read()
+        if numbers is None:
+            numbers = list(bands) if bands is not None else list(range(1, ds.bands + 1))
+            dtype = a.dtype
+            out_bands = np.zeros((K, len(numbers), P), dtype)
+        if a.dtype != dtype:
+            raise ValueError('%s: sample type %s differs from the stack\'s %s' % (fn, a.dtype, dtype))
+        if max(numbers) > ds.bands:
+            raise Exception('Band %s requested but raster only has %s bands' % (max(numbers),
+                                                                                 ds.bands))
+        idx, ok = grid_offsets(ds.geotransform(), (ds.height, ds.width), lng, lat)
+        planes = a.reshape(ds.bands, -1)
+        out_bands[k] = planes[[b - 1 for b in numbers]][:, idx] * ok
+        v = ok.copy()
+        if mask_fns[k]:
+            mds = _open(mask_fns[k])
+            midx, mok = grid_offsets(mds.geotransform(), (mds.height, mds.width), lng, lat)
+            mval = mds.read()[0].reshape(-1)[midx]
+            v &= ~(mok & (mval == 0))
+        valid[k] = v
+        dates.append(filename2date(fn))
+    return dict(dates=dates, bands=out_bands, band_numbers=numbers, valid=valid, n_pix=P)

@@ -1,0 +1,200 @@
+"""Local job orchestration: MRLandTrendrJob.steps (mr_land_trendr_job.py:154-159)
+without mrjob, EMR or S3, over a job directory laid out like the reference's S3 keys
+(settings.py:19-25):
+
+    <root>/<job>/input/settings.json             IN_SETTINGS
+    <root>/<job>/input/rasters/<...ledaps...>    IN_RASTS (analysis rasters: .tif, .tif.tar.gz, .zip)
+    <root>/<job>/input/rasters/<...cloudmask...> optional masks, same name with the trigger swapped
+    <root>/<job>/output/pix_grid.csv             OUT_GRID
+    <root>/<job>/output/rasters/<key>.tif        OUT_RAST_KEYNAME
+
+Steps, as the reference chains them:
+  1. setup    (setup_mapper :20-45)   analysis rasters by RAST_TRIGGER, grid from the first one;
+  2. parse    (parse_mapper :47-81)   ingest.ingest_stack: band samples + mask validity per grid
+                                      point (index_eqn runs on the GPU in step 3);
+  3. analysis (analysis_reducer :83-126) utils.analysis_reducer_batch over pixel tiles on the GPU;
+  4. output   (output_reducer :128-152) raster.label_rasters / trendline_rasters placed by each
+                                      grid point's template offsets, written as GeoTIFFs.
+
+Errors follow the reference: a pixel the reference's analysis raises for fails the job with the
+same exception type (on_error='raise'); on_error='skip' leaves such pixels NODATA instead.
+Grid points with no observation at all never reach the reference's reducer; they stay NODATA.
+
+CLI: python -m land_trendr_amd.job --root DIR --job NAME [--tile-pixels N] [--no-trendline]
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+from . import _abi
+from .ingest import (analysis_rasters, grid_points, grid_offsets, ingest_stack, mask_name,
+                     rast2grid, rast_local, read_grid)
+
+IN_SETTINGS = '%s/input/settings.json'
+IN_RASTS = '%s/input/rasters/'
+OUT_GRID = '%s/output/pix_grid.csv'
+OUT_RASTS = '%s/output/rasters/'
+
+
+class LocalJob:
+    def __init__(self, root, job, device=None, tile_pixels=1 << 22, trendline=True,
+                 raster_mode='reference', pre_threshold_mode='reference', on_error='raise',
+                 work_dir=None):
+        if on_error not in ('raise', 'skip'):
+            raise ValueError('on_error must be "raise" or "skip"')
+        self.root, self.job, self.device = root, job, device
+        self.tile_pixels = int(tile_pixels)
+        self.trendline = trendline
+        self.raster_mode = raster_mode
+        self.pre_threshold_mode = pre_threshold_mode
+        self.on_error = on_error
+        self.work_dir = work_dir or os.path.join(root, job, 'work')
+        self.settings_path = os.path.join(root, IN_SETTINGS % job)
+        self.grid_fn = os.path.join(root, OUT_GRID % job)
+        self.out_dir = os.path.join(root, OUT_RASTS % job)
+
+    def _path(self, key):
+        return os.path.join(self.root, key)
+
+    # 1. setup_mapper
+    def setup(self):
+        rdir = os.path.join(self.root, IN_RASTS % self.job)
+        names = sorted(os.listdir(rdir)) if os.path.isdir(rdir) else []
+        rasts = analysis_rasters(names)
+        if not rasts:
+            raise Exception('No analysis rasters specified for job %s' % self.job)
+        os.makedirs(self.work_dir, exist_ok=True)
+        self.rast_fns, self.mask_fns = [], []
+        for n in rasts:
+            self.rast_fns.append(rast_local(os.path.join(rdir, n), self.work_dir))
+            m = mask_name(n)
+            mp = os.path.join(rdir, m)
+            # parse_mapper: a mask that cannot be fetched is ignored (:59-63)
+            self.mask_fns.append(rast_local(mp, self.work_dir) if m != n and os.path.exists(mp)
+                                 else None)
+        os.makedirs(os.path.dirname(self.grid_fn), exist_ok=True)
+        rast2grid(self.rast_fns[0], out_csv=self.grid_fn)
+        with open(self.settings_path) as f:
+            self.settings = json.load(f)
+        return self.rast_fns
+
+    # 2. parse_mapper
+    def parse(self):
+        from .index_eqn import parse_eqn_bands
+        eqn_bands = sorted(parse_eqn_bands(self.settings['index_eqn']))
+        self.stack = ingest_stack(self.rast_fns, self.grid_fn, self.mask_fns, bands=eqn_bands)
+        return self.stack
+
+    # 3. analysis_reducer, batched over pixel tiles
+    def analyze(self):
+        import torch
+        from .engine import LABELS, TRENDLINE
+        from .utils import analysis_reducer_batch
+        st = self.stack
+        P = st['n_pix']
+        fields = LABELS + ('status', 'n_years') + (TRENDLINE if self.trendline else ('winner',))
+        dev = torch.device('cuda', self.device if self.device is not None else
+                           torch.cuda.current_device())
+        host = None
+        for p0 in range(0, P, self.tile_pixels):
+            p1 = min(P, p0 + self.tile_pixels)
+            bands = torch.from_numpy(np.ascontiguousarray(st['bands'][:, :, p0:p1])).to(dev)
+            valid = torch.from_numpy(np.ascontiguousarray(st['valid'][:, p0:p1])).to(dev)
+            out = analysis_reducer_batch(st['dates'], None, valid, self.settings, fields,
+                                         self.pre_threshold_mode, device=dev, bands=bands,
+                                         band_numbers=st['band_numbers'])
+            self.scene, self.rules = out.pop('_scene'), out.pop('_rules')
+            if host is None:
+                host = {k: np.empty(t.shape[:-1] + (P,), t.cpu().numpy().dtype)
+                        for k, t in out.items()}
+            for k, t in out.items():
+                host[k][..., p0:p1] = t.cpu().numpy()
+        self.planes = host
+        self._check_errors()
+        return host
+
+    def _check_errors(self):
+        from .utils import _raise_for_status
+        status = self.planes['status']
+        bad = np.flatnonzero(status & ~_abi.LT_ST_EMPTY)
+        if len(bad) == 0:
+            return
+        if self.on_error == 'raise':
+            p = int(bad[0])
+            wkt = read_grid(self.grid_fn)[p]
+            s = int(status[p])
+            if s & _abi.LT_ST_PRE_THRESHOLD_ATTR:
+                raise AttributeError("LabelRule instance has no attribute 'threshold' (pixel %s)"
+                                     % wkt)
+            try:
+                _raise_for_status(s, None)
+            except Exception as e:
+                raise type(e)('%s (pixel %s)' % (e, wkt)) from e
+        else:  # skip: the failing pixels emit nothing
+            self.planes['matched'][:, bad] = 0
+            if 'winner' in self.planes:
+                self.planes['winner'][:, bad] = -1
+
+    # 4. output_reducer
+    def output(self):
+        from .geotiff import GeoTiff
+        from .raster import label_rasters, output_reducer, trendline_rasters
+        tmpl = GeoTiff(self.rast_fns[0])
+        rows, cols = tmpl.height, tmpl.width
+        lng, lat = grid_points(self.grid_fn)
+        dest, ok = grid_offsets(tmpl.geotransform(), (rows, cols), lng, lat)
+        if not ok.all():
+            # data2raster assigns holder[y_off, x_off]: an off-template point raises there
+            raise IndexError('grid point %s is off the template raster'
+                             % read_grid(self.grid_fn)[int(np.flatnonzero(~ok)[0])])
+        n = rows * cols
+        placed = {}
+        empty = self.planes['status'] & _abi.LT_ST_EMPTY
+        for k, a in self.planes.items():
+            fill = -1 if k == 'winner' else 0
+            b = np.full(a.shape[:-1] + (n,), fill, a.dtype)
+            src = a
+            if k == 'matched':
+                src = np.where(empty[None, :] != 0, 0, a).astype(a.dtype)
+            b[..., dest] = src  # repeated offsets: the last grid point wins, as in the loop
+            placed[k] = b
+        tdt = tmpl.dtype.newbyteorder('=')
+        rasters = label_rasters(placed, self.rules, (rows, cols), tdt, self.raster_mode)
+        if self.trendline:
+            rasters.update(trendline_rasters(placed, self.scene, self.scene.dates, (rows, cols),
+                                             tdt, self.raster_mode))
+        return dict(output_reducer(rasters, tmpl, self.root, self.job))
+
+    def run(self):
+        self.setup()
+        self.parse()
+        self.analyze()
+        return self.output()
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description='LandTrendr job on the local GPU (steps of '
+                                 'MRLandTrendrJob without mrjob/S3)')
+    ap.add_argument('--root', required=True, help='directory holding <job>/input/...')
+    ap.add_argument('--job', required=True)
+    ap.add_argument('--device', type=int, default=None)
+    ap.add_argument('--tile-pixels', type=int, default=1 << 22)
+    ap.add_argument('--no-trendline', action='store_true')
+    ap.add_argument('--raster-mode', choices=('reference', 'typed'), default='reference')
+    ap.add_argument('--pre-threshold-mode', choices=('reference', 'documented'),
+                    default='reference')
+    ap.add_argument('--on-error', choices=('raise', 'skip'), default='raise')
+    a = ap.parse_args(argv)
+    j = LocalJob(a.root, a.job, a.device, a.tile_pixels, not a.no_trendline, a.raster_mode,
+                 a.pre_threshold_mode, a.on_error)
+    res = j.run()
+    for key in sorted(res):
+        print('%s\t%s' % (key, res[key][0]))
+    return 0
+
+
+if __name__ == '__main__':
+    sys.exit(main())

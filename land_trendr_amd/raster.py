@@ -124,75 +124,87 @@ _SAMPLE_FORMAT = {'u': 1, 'i': 2, 'f': 3}
 _GEO_TAGS = (33550, 33922, 34264, 34735, 34736, 34737)  # scale, tiepoint, transform, geokeys ...
 
 
-def write_geotiff(path, array, template=None, nodata=NODATA):
-    """Single-band, uncompressed, little-endian GeoTIFF of a 2-D array; georeferencing tags copied
-    verbatim from `template` (a GeoTiff or a path), GDAL_NODATA set to `nodata`."""
+def write_geotiff(path, array, template=None, nodata=NODATA, geotransform=None):
+    """Uncompressed little-endian GeoTIFF of a 2-D array, or of a 3-D [bands, rows, cols] array
+    (planar configuration 2: one strip per band, what GeoTiff.read returns as [bands, rows, cols]);
+    georeferencing tags copied verbatim from `template` (a GeoTiff or a path), or written from a
+    north-up `geotransform` (ModelPixelScale + ModelTiepoint), GDAL_NODATA set to `nodata`."""
     a = np.ascontiguousarray(array)
-    if a.ndim != 2 or a.dtype.kind not in _SAMPLE_FORMAT:
-        raise ValueError('write_geotiff: 2-D integer or float array required')
+    if a.ndim not in (2, 3) or a.dtype.kind not in _SAMPLE_FORMAT:
+        raise ValueError('write_geotiff: 2-D or 3-D integer or float array required')
     a = a.astype(a.dtype.newbyteorder('<'), copy=False)
-    rows, cols = a.shape
+    if a.ndim == 2:
+        a = a[None]
+    nb, rows, cols = a.shape
     tmpl = GeoTiff(template) if isinstance(template, str) else template
-    entries = []  # (tag, type, count, payload bytes)
+    plane = rows * cols * a.dtype.itemsize
 
-    def add(tag, typ, values, fmt):
-        payload = struct.pack('<' + fmt * len(values), *values)
-        entries.append((tag, typ, len(values), payload))
+    def layout(data_off):
+        entries = []  # (tag, type, count, payload bytes)
 
-    add(256, 4, [cols], 'I')
-    add(257, 4, [rows], 'I')
-    add(258, 3, [a.dtype.itemsize * 8], 'H')
-    add(259, 3, [1], 'H')
-    add(262, 3, [1], 'H')
-    data = a.tobytes()
-    add(273, 4, [0], 'I')  # patched below
-    add(277, 3, [1], 'H')
-    add(278, 4, [rows], 'I')
-    add(279, 4, [len(data)], 'I')
-    add(284, 3, [1], 'H')
-    add(339, 3, [_SAMPLE_FORMAT[a.dtype.kind]], 'H')
-    if tmpl is not None:
-        for tag in _GEO_TAGS:
-            if tag in tmpl.tags:
-                v = tmpl.tags[tag]
-                if isinstance(v, str):
-                    entries.append((tag, 2, len(v), v.encode('latin-1')))
-                elif tag == 34735:
-                    add(tag, 3, [int(x) for x in v], 'H')
-                else:
-                    add(tag, 12, [float(x) for x in v], 'd')
-    if nodata is not None:
-        s = ('%g' % nodata).encode() + b'\x00'
-        entries.append((42113, 2, len(s), s))
-    entries.sort(key=lambda e: e[0])
-    n = len(entries)
-    ifd_off = 8
-    extra_off = ifd_off + 2 + 12 * n + 4
-    extra = b''
-    ifd = struct.pack('<H', n)
-    offsets = {}
-    for tag, typ, cnt, payload in entries:
-        if len(payload) <= 4:
-            ifd += struct.pack('<HHI', tag, typ, cnt) + payload.ljust(4, b'\x00')
-        else:
-            if len(extra) % 2:
-                extra += b'\x00'
-            offsets[tag] = extra_off + len(extra)
-            ifd += struct.pack('<HHII', tag, typ, cnt, offsets[tag])
-            extra += payload
-    ifd += struct.pack('<I', 0)
-    data_off = extra_off + len(extra)
-    data_off += (-data_off) % 8
-    # patch StripOffsets (tag 273, inline) with the data offset
-    k = [e[0] for e in entries].index(273)
-    pos = 2 + 12 * k + 8
-    ifd = ifd[:pos] + struct.pack('<I', data_off) + ifd[pos + 4:]
+        def add(tag, typ, values, fmt):
+            payload = struct.pack('<' + fmt * len(values), *values)
+            entries.append((tag, typ, len(values), payload))
+
+        add(256, 4, [cols], 'I')
+        add(257, 4, [rows], 'I')
+        add(258, 3, [a.dtype.itemsize * 8] * nb, 'H')
+        add(259, 3, [1], 'H')
+        add(262, 3, [1], 'H')
+        add(273, 4, [data_off + b * plane for b in range(nb)], 'I')
+        add(277, 3, [nb], 'H')
+        add(278, 4, [rows], 'I')
+        add(279, 4, [plane] * nb, 'I')
+        add(284, 3, [2 if nb > 1 else 1], 'H')
+        add(339, 3, [_SAMPLE_FORMAT[a.dtype.kind]] * nb, 'H')
+        if tmpl is not None:
+            for tag in _GEO_TAGS:
+                if tag in tmpl.tags:
+                    v = tmpl.tags[tag]
+                    if isinstance(v, str):
+                        entries.append((tag, 2, len(v), v.encode('latin-1')))
+                    elif tag == 34735:
+                        add(tag, 3, [int(x) for x in v], 'H')
+                    else:
+                        add(tag, 12, [float(x) for x in v], 'd')
+        elif geotransform is not None:
+            x0, sx, rx, y0, ry, sy = (float(v) for v in geotransform)
+            if rx != 0.0 or ry != 0.0:
+                raise ValueError('write_geotiff: rotated geotransforms are not supported')
+            add(33550, 12, [sx, -sy, 0.0], 'd')
+            add(33922, 12, [0.0, 0.0, 0.0, x0, y0, 0.0], 'd')
+        if nodata is not None:
+            s = ('%g' % nodata).encode() + b'\x00'
+            entries.append((42113, 2, len(s), s))
+        entries.sort(key=lambda e: e[0])
+        n = len(entries)
+        ifd_off = 8
+        extra_off = ifd_off + 2 + 12 * n + 4
+        extra = b''
+        ifd = struct.pack('<H', n)
+        for tag, typ, cnt, payload in entries:
+            if len(payload) <= 4:
+                ifd += struct.pack('<HHI', tag, typ, cnt) + payload.ljust(4, b'\x00')
+            else:
+                if len(extra) % 2:
+                    extra += b'\x00'
+                ifd += struct.pack('<HHII', tag, typ, cnt, extra_off + len(extra))
+                extra += payload
+        ifd += struct.pack('<I', 0)
+        end = extra_off + len(extra)
+        return ifd_off, ifd, extra, end + (-end) % 8
+
+    # the header's size does not depend on the offset values: lay out once to find where the
+    # pixel data starts, then again with the real strip offsets
+    data_off = layout(0)[3]
+    ifd_off, ifd, extra, end = layout(data_off)
+    assert end == data_off
     with open(path, 'wb') as f:
         f.write(b'II*\x00' + struct.pack('<I', ifd_off))
         f.write(ifd)
         f.write(extra)
-        f.write(b'\x00' * (data_off - extra_off - len(extra)))
-        f.write(data)
+        f.write(b'\x00' * (data_off - ifd_off - len(ifd) - len(extra)))
+        f.write(a.tobytes())
     return path
 
 
