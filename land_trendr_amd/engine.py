@@ -193,6 +193,8 @@ _ENGINES = {}
 
 
 def get_engine(device=None):
+    if isinstance(device, torch.device):
+        device = device.index
     idx = torch.cuda.current_device() if device is None else int(device)
     eng = _ENGINES.get(idx)
     if eng is None:
