@@ -268,10 +268,21 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
           const double yj = (double)L.ys[j][lane];
           SyyAll = __builtin_fma(yj, yj, SyyAll);
         }
+        // the next start's operands are loaded one iteration ahead, so the LDS and private-memory
+        // latency overlaps this start's arithmetic
+        int xpre = L.xn[j][lane];
+        VT ypre = L.ys[j][lane];
+        double opre = OPT[j];
         for (int ii = j; ii >= 0; ii--) {
           const int i = __builtin_amdgcn_readfirstlane(ii);  // wave-uniform start
-          const int xi = L.xn[i][lane];
-          const double yi = (double)L.ys[i][lane];
+          const int xi = xpre;
+          const double yi = (double)ypre;
+          const double oi = opre;
+          if (i > 0) {
+            xpre = L.xn[i - 1][lane];
+            ypre = L.ys[i - 1][lane];
+            opre = OPT[i - 1];
+          }
           Sx += xi;
           Sxx += xi * xi;
           Sy += yi;
@@ -290,12 +301,12 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
             e = __builtin_fma(t1, D, -(N1 * N1)) * r;
             e = e < 0.0 ? 0.0 : e;
           }
-          const double v = (e + c) + OPT[i];
+          const double v = (e + c) + oi;
           if (m >= 3) w = __builtin_fma(0x1p-50, __builtin_fabs(v), kScreen * Syy);
           if (v - w <= H) cand |= 1ull << i;
           H = v + w < H ? v + w : H;
           // early exit (dp_start_bound): no start below i can reach H
-          if (prune && m >= 3 && !__ballot(col && !(dp_start_bound(e, OPT[i], 0.0, c, SyyAll) > H)))
+          if (prune && m >= 3 && !__ballot(col && !(dp_start_bound(e, oi, 0.0, c, SyyAll) > H)))
             break;
         }
         const int nc = col ? __builtin_popcountll(cand) : 0;
@@ -306,6 +317,7 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
           const bool act = r < nc;
           const int i = act ? __builtin_ctzll(cand) : 0;
           if (act) cand &= cand - 1;
+          const double oi = OPT[i];  // per-lane index, loaded before the fit that hides it
           const int m = j - i + 1;
           const bool ls = act && m >= 3;
           double e = 0.0;
@@ -319,7 +331,7 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
               e = ssr;
             }
           }
-          const double v = (e + c) + OPT[i];  // per-lane index
+          const double v = (e + c) + oi;
           if (act && v < best) {  // increasing start order + strict "<": the first minimum
             best = v;
             bi = i;
@@ -483,10 +495,21 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
         const double yj = (double)L.ys[j][lane];
         SyyAll = __builtin_fma(yj, yj, SyyAll);
       }
+      // the next start's operands are loaded one iteration ahead, so the LDS and private-memory
+      // latency overlaps this start's arithmetic (OPTa[0..j] are all written)
+      int xpre = L.xn[j][lane];
+      VT ypre = L.ys[j][lane];
+      double opre = OPTa[j];
       for (int ii = j; ii >= 0; ii--) {
         const int i = __builtin_amdgcn_readfirstlane(ii);  // wave-uniform start
-        const int xi = L.xn[i][lane];
-        const double yi = (double)L.ys[i][lane];
+        const int xi = xpre;
+        const double yi = (double)ypre;
+        const double oi = opre;
+        if (i > 0) {
+          xpre = L.xn[i - 1][lane];
+          ypre = L.ys[i - 1][lane];
+          opre = OPTa[i - 1];
+        }
         Sx += xi;
         Sxx += xi * xi;
         Sy += yi;
@@ -503,7 +526,7 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
         double r = __builtin_amdgcn_rcp(den);
         r = __builtin_fma(r, __builtin_fma(-den, r, 1.0), r);
         const double e = __builtin_fmax(__builtin_fma(t1, D, -(N1 * N1)) * r, 0.0);
-        const double v = (e + c) + OPTa[i];
+        const double v = (e + c) + oi;
         // interval around the reference value: OPT bound + screening bound of this segment +
         // the rounding of this candidate's own two additions
         const double wopt = ((exact >> i) & 1) ? 0.0 : Emax;
@@ -522,7 +545,7 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
         // any lane, the column is complete
         if (prune) {
           const double Hb = Hi < Ve ? Hi : Ve;
-          if (!__ballot(col && !(dp_start_bound(e, OPTa[i], wopt, c, SyyAll) > Hb))) break;
+          if (!__ballot(col && !(dp_start_bound(e, oi, wopt, c, SyyAll) > Hb))) break;
         }
       }
       const double H = Hi < Ve ? Hi : Ve;  // the exact minimum lies in [min(L1, Ve), H]
