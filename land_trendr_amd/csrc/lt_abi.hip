@@ -60,7 +60,7 @@ __global__ __launch_bounds__(64) void analyze_fast_kernel(const lt::DevScene* __
                                                           const lt::lsq_xf* __restrict__ xtab,
                                                           int64_t* __restrict__ defer,
                                                           unsigned long long* __restrict__ n_defer) {
-  __shared__ lt::WaveLds<MAXY, float> L;
+  __shared__ lt::WaveLds<MAXY, float, false> L;
   const int lane = threadIdx.x;
   const int64_t p = (int64_t)blockIdx.x * 64 + lane;
   const bool live = p < in.n_pix;
@@ -81,7 +81,7 @@ __global__ __launch_bounds__(64) void resolve_fast_kernel(const lt::DevScene* __
                                                           const lt::lsq_xf* __restrict__ xtab,
                                                           const int64_t* __restrict__ defer,
                                                           unsigned long long* __restrict__ counters) {
-  __shared__ lt::WaveLds<MAXY, VT> L;
+  __shared__ lt::WaveLds<MAXY, VT, true> L;
   const int lane = threadIdx.x;
   const int64_t n = (int64_t)counters[0];  // written by stage 1, a previous launch
   for (;;) {
@@ -362,6 +362,10 @@ int lt_analyze_tile(lt_ctx* c, const lt_scene* sc, const lt_params* prm, const l
 #define LT_LAUNCH_FAST(MY, RM)                                                              \
   hipLaunchKernelGGL((analyze_fast_kernel<MY, RM>), fgrid, fblock, 0, stream, c->d_scene, *prm, \
                      *in, *out, c->d_xtab, c->d_defer, c->d_ndefer)
+#ifdef LT_DEV_ONE_CONFIG  // assembly-inspection builds only (-S): the c2 instances alone
+  (void)one; (void)few;
+  LT_LAUNCH_FAST(32, 1);
+#else
   if (Y <= 32) {
     if (one) LT_LAUNCH_FAST(32, 1); else if (few) LT_LAUNCH_FAST(32, 4); else LT_LAUNCH_FAST(32, 16);
   } else if (Y <= 48) {
@@ -369,6 +373,7 @@ int lt_analyze_tile(lt_ctx* c, const lt_scene* sc, const lt_params* prm, const l
   } else {
     if (one) LT_LAUNCH_FAST(64, 1); else if (few) LT_LAUNCH_FAST(64, 4); else LT_LAUNCH_FAST(64, 16);
   }
+#endif
 #undef LT_LAUNCH_FAST
   HIP_OR_FAIL(c, hipGetLastError());
   if (ep[0]) HIP_OR_FAIL(c, hipEventRecord(ep[0]->stop, stream));
@@ -385,6 +390,9 @@ int lt_analyze_tile(lt_ctx* c, const lt_scene* sc, const lt_params* prm, const l
     LT_LAUNCH_RESOLVE1(MY, RM, float, c->d_defer, c->d_ndefer);                             \
     LT_LAUNCH_RESOLVE1(MY, RM, double, c->d_defer + in->n_pix, c->d_ndefer + 2);            \
   } while (0)
+#ifdef LT_DEV_ONE_CONFIG
+  LT_LAUNCH_RESOLVE(32, 1);
+#else
   if (Y <= 32) {
     if (one) LT_LAUNCH_RESOLVE(32, 1); else if (few) LT_LAUNCH_RESOLVE(32, 4); else LT_LAUNCH_RESOLVE(32, 16);
   } else if (Y <= 48) {
@@ -392,6 +400,7 @@ int lt_analyze_tile(lt_ctx* c, const lt_scene* sc, const lt_params* prm, const l
   } else {
     if (one) LT_LAUNCH_RESOLVE(64, 1); else if (few) LT_LAUNCH_RESOLVE(64, 4); else LT_LAUNCH_RESOLVE(64, 16);
   }
+#endif
 #undef LT_LAUNCH_RESOLVE
 #undef LT_LAUNCH_RESOLVE1
   HIP_OR_FAIL(c, hipGetLastError());

@@ -54,11 +54,14 @@ __device__ inline int lsq_lockstep(bool act, int m, GX X, GY Y, const lsq_xf* __
 
 // VT: storage type of the series. The analyze stage stores binary32 (pixels whose values are not
 // exact in binary32 are sent to the resolve stage), the resolve stage binary64.
-template <int MAXY, class VT>
+// AGLDS: the DP argmin of each column in LDS (resolve stage: its registers are spent on the exact
+// DP) or, when false, in the lane's registers / private memory (analyze stage: 2 KB less LDS per
+// wave, 15 instead of 12 resident waves per CU)
+template <int MAXY, class VT, bool AGLDS>
 struct WaveLds {
   VT ys[MAXY][64];       // present values (t), compacted in place to non-spike (k)
   uint8_t xn[MAXY][64];  // year offset of non-spike point k
-  uint8_t ag[MAXY][64];  // DP argmin of column k; after the backtrack: non-spike index of vertex q
+  uint8_t ag[AGLDS ? MAXY : 1][64];  // DP argmin of column k (AGLDS only)
   int32_t year[LT_MAX_YEARS];  // the scene's calendar year per slot (64 words: one bank each)
 };
 
@@ -71,7 +74,7 @@ enum { kDone = 0, kDeferExact = 1, kDeferWide = 2 };
 template <int MAXY, int RMAX, bool EXACT, class VT>
 __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const lt_tile_in& in,
                                    const lt_tile_out& out, const lsq_xf* __restrict__ xtab,
-                                   int64_t p, bool live, int lane, WaveLds<MAXY, VT>& L) {
+                                   int64_t p, bool live, int lane, WaveLds<MAXY, VT, EXACT>& L) {
   const int Y = S.n_years;
   const int64_t is = in.stride, os = out.stride;
   const double nan = __builtin_nan("");
@@ -244,6 +247,17 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
   // ---- segmented least squares DP (utils.py:618-631), decided lazily ----
   bool deferred = live && T >= 2 && f32_bad;
   uint64_t vmask = 0;  // vertices over non-spike indices
+  // DP argmin of each column (see WaveLds): written at wave-uniform columns, read once per vertex
+  // by the backtrack
+  uint8_t AG[EXACT ? 1 : MAXY];
+  auto ag_set = [&](int j, int a) {
+    if constexpr (EXACT) L.ag[j][lane] = (uint8_t)a;
+    else AG[j] = (uint8_t)a;
+  };
+  auto ag_get = [&](int j) -> int {
+    if constexpr (EXACT) return L.ag[j][lane];
+    else return AG[j];
+  };
   if constexpr (EXACT) {
     if constexpr (MAXY <= 32) {
       // ---- exact-OPT DP: closed-form intervals, then the emulated LAPACK residual for every
@@ -338,7 +352,7 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
           }
         }
         if (col) {
-          L.ag[j][lane] = (uint8_t)bi;
+          ag_set(j, bi);
           OPT[j + 1] = best;
         }
       }
@@ -428,7 +442,7 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
           }
         }
         if (col) {
-          L.ag[j][lane] = (uint8_t)bi;
+          ag_set(j, bi);
 #pragma unroll
           for (int k = 1; k <= MAXY; k++)
             if (k == j + 1) OPT[k] = best;  // wave-uniform index
@@ -438,7 +452,7 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
     if (n >= 1) {
       vmask = 1ull << (n - 1);
       for (int j = n - 1; j >= 0;) {
-        const int a = L.ag[j][lane];
+        const int a = ag_get(j);
         vmask |= 1ull << a;
         j = a - 1;
       }
@@ -495,27 +509,18 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
         const double yj = (double)L.ys[j][lane];
         SyyAll = __builtin_fma(yj, yj, SyyAll);
       }
-      // the next start's operands are loaded one iteration ahead, so the LDS and private-memory
-      // latency overlaps this start's arithmetic (OPTa[0..j] are all written)
-      int xpre = L.xn[j][lane];
-      VT ypre = L.ys[j][lane];
-      double opre = OPTa[j];
-      for (int ii = j; ii >= 0; ii--) {
-        const int i = __builtin_amdgcn_readfirstlane(ii);  // wave-uniform start
-        const int xi = xpre;
-        const double yi = (double)ypre;
-        const double oi = opre;
-        if (i > 0) {
-          xpre = L.xn[i - 1][lane];
-          ypre = L.ys[i - 1][lane];
-          opre = OPTa[i - 1];
-        }
+      auto add_point = [&](int i) {
+        const int xi = L.xn[i][lane];
+        const double yi = (double)L.ys[i][lane];
         Sx += xi;
         Sxx += xi * xi;
         Sy += yi;
         Sxy = __builtin_fma((double)xi, yi, Sxy);
         Syy = __builtin_fma(yi, yi, Syy);
-        if (i + 2 > j) continue;  // the 1- and 2-point starts are priced above
+      };
+      // start i (>= 3 points) priced from the current sums: value v, its interval [lo, hi] around
+      // the reference value, and the early-exit bound for the starts below it
+      auto price = [&](int i, double& v, double& hi, double& lo, double& bnd) {
         // closed-form SSE: (m*Syy - Sy^2 - N1^2/D) / m, one reciprocal
         const int m = j - i + 1;  // wave-uniform, >= 3
         const double md = (double)m;
@@ -526,12 +531,18 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
         double r = __builtin_amdgcn_rcp(den);
         r = __builtin_fma(r, __builtin_fma(-den, r, 1.0), r);
         const double e = __builtin_fmax(__builtin_fma(t1, D, -(N1 * N1)) * r, 0.0);
-        const double v = (e + c) + oi;
+        const double o = OPTa[i];
+        v = (e + c) + o;
         // interval around the reference value: OPT bound + screening bound of this segment +
         // the rounding of this candidate's own two additions
         const double wopt = ((exact >> i) & 1) ? 0.0 : Emax;
         const double w = __builtin_fma(0x1p-50, __builtin_fabs(v), __builtin_fma(kScreen, Syy, wopt));
-        const double hi = v + w, lo = v - w;
+        hi = v + w;
+        lo = v - w;
+        bnd = dp_start_bound(e, o, wopt, c, SyyAll);
+      };
+      // candidates in decreasing start order ("<=" keeps the smaller start among equal values)
+      auto track = [&](int i, double v, double hi, double lo) {
         if (hi <= Hi) {
           i1 = i;
           v1 = v;
@@ -541,11 +552,29 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
         L2 = bl ? L1 : (lo < L2 ? lo : L2);
         L1 = bl ? lo : L1;
         iL = bl ? i : iL;
-        // early exit (dp_start_bound): once no start below i can reach the best upper end in
-        // any lane, the column is complete
+      };
+      // the 1- and 2-point starts (priced above) only add their points to the sums
+      add_point(j);
+      if (j >= 1) add_point(j - 1);
+      // the other starts two at a time: two independent pricing chains per iteration and one
+      // exit test. Early exit (dp_start_bound): once no start below i can reach an upper bound on
+      // the column minimum in any lane, the column is complete; a start priced past that point
+      // lies above the bound, so tracking it changes no decision
+      for (int ii = j - 2; ii >= 0; ii -= 2) {
+        const int i = __builtin_amdgcn_readfirstlane(ii);  // wave-uniform start
+        const bool two = i >= 1;                            // wave-uniform
+        add_point(i);
+        double va, ha, la, ba, vb = 0.0, hb = 0.0, lb = 0.0, bb = 0.0;
+        price(i, va, ha, la, ba);
+        if (two) {
+          add_point(i - 1);
+          price(i - 1, vb, hb, lb, bb);
+        }
+        track(i, va, ha, la);
+        if (two) track(i - 1, vb, hb, lb);
         if (prune) {
           const double Hb = Hi < Ve ? Hi : Ve;
-          if (!__ballot(col && !(dp_start_bound(e, oi, wopt, c, SyyAll) > Hb))) break;
+          if (!__ballot(col && !(ba > Hb || (two && bb > Hb)))) break;
         }
       }
       const double H = Hi < Ve ? Hi : Ve;  // the exact minimum lies in [min(L1, Ve), H]
@@ -569,7 +598,7 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
         enew = (H - Lo) * (1.0 + 0x1p-40) + 0x1p-50 * __builtin_fabs(vnew);
       }
       if (col) {
-        L.ag[j][lane] = (uint8_t)a;
+        ag_set(j, a);
         OPTa[j + 1] = vnew;  // wave-uniform index
         if (exnew) exact |= 2ull << j;
         Emax = enew > Emax ? enew : Emax;
@@ -581,7 +610,7 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
     if (n >= 1) {
       vmask = 1ull << (n - 1);
       for (int j = n - 1; j >= 0;) {
-        const int a = L.ag[j][lane];
+        const int a = ag_get(j);
         if ((amb >> j) & 1) deferred = true;
         vmask |= 1ull << a;
         j = a - 1;
@@ -592,9 +621,9 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
   if (deferred) vmask = 0;
 
   // ---- vertices2eqns + eqns2fitted_points in lockstep over the vertex number q ----
-  int nv = 0;
-  for (uint64_t m = vmask; m; m &= m - 1) L.ag[nv++][lane] = (uint8_t)__builtin_ctzll(m);
+  const int nv = __builtin_popcountll(vmask);
   const int nvmax = wave_max(nv);
+  uint64_t vrem = vmask;  // vertices from q on: vertex q is its lowest bit
   double pm = 0.0, pb = 0.0;   // eqn of vertex q-1
   RuleState1 rs[RMAX];
   double prev_fit = 0.0;
@@ -603,9 +632,10 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
   uint64_t wrem = pres;        // year slots of the present points from ta on
   for (int q = 0; q < nvmax; q++) {
     const bool act = q < nv;
-    const int ka = act ? L.ag[q][lane] : 0;
+    const int ka = act ? __builtin_ctzll(vrem) : 0;
+    if (act) vrem &= vrem - 1;
     const bool has_next = act && q + 1 < nv;
-    const int kb = has_next ? L.ag[q + 1][lane] : ka;
+    const int kb = has_next ? __builtin_ctzll(vrem) : ka;
     double cm = pm, cb = pb;
     // one LAPACK-emulated fit per vertex number for the whole wave (lanes without a next
     // vertex reuse the previous equation, utils.py:662)
