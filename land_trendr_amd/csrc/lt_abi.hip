@@ -54,7 +54,7 @@ __device__ inline void defer_append(bool deferred, int64_t p, int lane, int64_t*
 
 // Stage 1 (wave-lockstep body, lt_fast.h): one wave per workgroup, the pixel series in LDS.
 template <int MAXY, int RMAX>
-__global__ __launch_bounds__(64) void analyze_fast_kernel(const lt::DevScene* __restrict__ S,
+__global__ __launch_bounds__(64, 4) void analyze_fast_kernel(const lt::DevScene* __restrict__ S,
                                                           const lt_params P, const lt_tile_in in,
                                                           const lt_tile_out out,
                                                           const lt::lsq_xf* __restrict__ xtab,

@@ -464,7 +464,12 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
     OPTa[0] = 0.0;
     uint64_t exact = 1;      // bit k: OPTa[k] is the reference value itself
     double Emax = 0.0;       // bound on |OPTa[k] - OPT[k]| for every inexact k so far
-    double opt_j = 0.0, opt_jm1 = 0.0;  // OPTa[j] and OPTa[j-1] (the 1- and 2-point starts)
+    // register window of the four most recent points (x, y of points j..j-3) and of OPTa[j..j-3]:
+    // the 1- to 4-point starts of a column, nearly all the DP prices, read no LDS or private
+    // memory
+    double opt_j = 0.0, opt_jm1 = 0.0, opt_jm2 = 0.0, opt_jm3 = 0.0;
+    int wx0 = 0, wx1 = 0, wx2 = 0, wx3 = 0;
+    double wy0 = 0.0, wy1 = 0.0, wy2 = 0.0, wy3 = 0.0;
     double SyyAll = 0.0;                // sum of y^2 over the points 0..j
     const bool prune = c >= 0.0;
     uint64_t amb = 0;
@@ -505,13 +510,16 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
         }
       }
       // prefix bound for the early exit below: every segment ending at j has Syy <= SyyAll
-      {
-        const double yj = (double)L.ys[j][lane];
-        SyyAll = __builtin_fma(yj, yj, SyyAll);
-      }
-      auto add_point = [&](int i) {
-        const int xi = L.xn[i][lane];
-        const double yi = (double)L.ys[i][lane];
+      wx3 = wx2;
+      wx2 = wx1;
+      wx1 = wx0;
+      wx0 = L.xn[j][lane];
+      wy3 = wy2;
+      wy2 = wy1;
+      wy1 = wy0;
+      wy0 = (double)L.ys[j][lane];
+      SyyAll = __builtin_fma(wy0, wy0, SyyAll);
+      auto add_xy = [&](int xi, double yi) {
         Sx += xi;
         Sxx += xi * xi;
         Sy += yi;
@@ -520,7 +528,7 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
       };
       // start i (>= 3 points) priced from the current sums: value v, its interval [lo, hi] around
       // the reference value, and the early-exit bound for the starts below it
-      auto price = [&](int i, double& v, double& hi, double& lo, double& bnd) {
+      auto price = [&](int i, double o, double& v, double& hi, double& lo, double& bnd) {
         // closed-form SSE: (m*Syy - Sy^2 - N1^2/D) / m, one reciprocal
         const int m = j - i + 1;  // wave-uniform, >= 3
         const double md = (double)m;
@@ -531,8 +539,7 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
         double r = __builtin_amdgcn_rcp(den);
         r = __builtin_fma(r, __builtin_fma(-den, r, 1.0), r);
         const double e = __builtin_fmax(__builtin_fma(t1, D, -(N1 * N1)) * r, 0.0);
-        const double o = OPTa[i];
-        v = (e + c) + o;
+        v = (e + c) + o;  // o = OPTa[i]
         // interval around the reference value: OPT bound + screening bound of this segment +
         // the rounding of this candidate's own two additions
         const double wopt = ((exact >> i) & 1) ? 0.0 : Emax;
@@ -554,21 +561,39 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
         iL = bl ? i : iL;
       };
       // the 1- and 2-point starts (priced above) only add their points to the sums
-      add_point(j);
-      if (j >= 1) add_point(j - 1);
+      add_xy(wx0, wy0);
+      if (j >= 1) add_xy(wx1, wy1);
       // the other starts two at a time: two independent pricing chains per iteration and one
       // exit test. Early exit (dp_start_bound): once no start below i can reach an upper bound on
       // the column minimum in any lane, the column is complete; a start priced past that point
       // lies above the bound, so tracking it changes no decision
-      for (int ii = j - 2; ii >= 0; ii -= 2) {
+      bool more = j >= 2;  // wave-uniform
+      if (more) {  // starts j-2 and j-3 from the register window
+        const bool two = j >= 3;
+        double va, ha, la, ba, vb = 0.0, hb = 0.0, lb = 0.0, bb = 0.0;
+        add_xy(wx2, wy2);
+        price(j - 2, opt_jm2, va, ha, la, ba);
+        if (two) {
+          add_xy(wx3, wy3);
+          price(j - 3, opt_jm3, vb, hb, lb, bb);
+        }
+        track(j - 2, va, ha, la);
+        if (two) track(j - 3, vb, hb, lb);
+        if (prune) {
+          const double Hb = Hi < Ve ? Hi : Ve;
+          if (!__ballot(col && !(ba > Hb || (two && bb > Hb)))) more = false;
+        }
+        more = more && two;
+      }
+      for (int ii = j - 4; more && ii >= 0; ii -= 2) {  // the rest from LDS / private memory
         const int i = __builtin_amdgcn_readfirstlane(ii);  // wave-uniform start
         const bool two = i >= 1;                            // wave-uniform
-        add_point(i);
+        add_xy(L.xn[i][lane], (double)L.ys[i][lane]);
         double va, ha, la, ba, vb = 0.0, hb = 0.0, lb = 0.0, bb = 0.0;
-        price(i, va, ha, la, ba);
+        price(i, OPTa[i], va, ha, la, ba);
         if (two) {
-          add_point(i - 1);
-          price(i - 1, vb, hb, lb, bb);
+          add_xy(L.xn[i - 1][lane], (double)L.ys[i - 1][lane]);
+          price(i - 1, OPTa[i - 1], vb, hb, lb, bb);
         }
         track(i, va, ha, la);
         if (two) track(i - 1, vb, hb, lb);
@@ -602,6 +627,8 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
         OPTa[j + 1] = vnew;  // wave-uniform index
         if (exnew) exact |= 2ull << j;
         Emax = enew > Emax ? enew : Emax;
+        opt_jm3 = opt_jm2;
+        opt_jm2 = opt_jm1;
         opt_jm1 = opt_j;
         opt_j = vnew;
       }
@@ -621,6 +648,9 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
   if (deferred) vmask = 0;
 
   // ---- vertices2eqns + eqns2fitted_points in lockstep over the vertex number q ----
+  // per-year planes requested (launch-uniform): otherwise the walk over the points is skipped
+  const bool year_out = out.val_fit || out.fit_m || out.fit_b || out.right_m || out.right_b ||
+                        out.spike || out.vertex;
   const int nv = __builtin_popcountll(vmask);
   const int nvmax = wave_max(nv);
   uint64_t vrem = vmask;  // vertices from q on: vertex q is its lowest bit
@@ -656,8 +686,18 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
     // present points from the vertex, counting non-spike ones until the next vertex
     const double raw_v = act ? (double)L.ys[ka][lane] : 0.0;
     double fit_vertex = 0.0;
+    if (!year_out) {  // labels only: the fitted value at the vertex is all the rules need
+      const double x = act ? (double)L.xn[ka][lane] : 0.0;  // the vertex's year offset
+      if (q > 0 && !(pm == cm && pb == cb)) {
+        const double fl = (pm * x) + pb;
+        const double fr = (cm * x) + cb;
+        fit_vertex = __builtin_fabs(fl - raw_v) <= __builtin_fabs(fr - raw_v) ? fl : fr;
+      } else {
+        fit_vertex = (cm * x) + cb;
+      }
+    }
     int t = ta, kk = ka;
-    bool going = act;
+    bool going = act && year_out;
     for (int s = 0; __ballot(going); s++) {
       if (!going) continue;
       if (s > 0) {

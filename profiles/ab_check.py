@@ -20,17 +20,21 @@ sc = make_scene(n, n_years=30, seed=int(sys.argv[2]) if len(sys.argv) > 2 else 1
 meta = build_scene(sc.dates, parse_date('2014-07-01'))
 params, _ = compile_params(10.0, [{'name': 'gd', 'val': 1, 'change_type': 'GD'}])
 eng = get_engine(0)
-out = eng.analyze_tile(meta, params, sc.values.to(eng.device), None)
-torch.cuda.synchronize()
-got = {k: t.cpu().numpy() for k, t in out.items()}
 exp = oracle.analyze_tile(meta, params, sc.values.numpy(), None, n_threads=16)
-bad = {}
-for k, a in got.items():
-    e = exp[k][:a.shape[0]] if a.ndim == 2 else exp[k]
-    if k in ('onset_year', 'duration', 'class_val', 'magnitude', 'initial_val'):
-        m = exp['matched'][:a.shape[0]].astype(bool)
-        a, e = np.where(m, a, 0), np.where(m, e, 0)
-    ok = _bits_equal(a, e) if a.dtype.kind == 'f' else (a == e)
-    if not ok.all():
-        bad[k] = int((~ok).sum())
-print('parity', n, 'px', 'OK' if not bad else bad)
+for fields in (None, ('status', 'n_years', 'matched', 'class_val', 'onset_year', 'duration',
+                      'magnitude', 'initial_val')):
+    out = (eng.analyze_tile(meta, params, sc.values.to(eng.device), None) if fields is None else
+           eng.analyze_tile(meta, params, sc.values.to(eng.device), None, fields))
+    torch.cuda.synchronize()
+    got = {k: t.cpu().numpy() for k, t in out.items()}
+    bad = {}
+    for k, a in got.items():
+        e = exp[k][:a.shape[0]] if a.ndim == 2 else exp[k]
+        if k in ('onset_year', 'duration', 'class_val', 'magnitude', 'initial_val'):
+            m = exp['matched'][:a.shape[0]].astype(bool)
+            a, e = np.where(m, a, 0), np.where(m, e, 0)
+        ok = _bits_equal(a, e) if a.dtype.kind == 'f' else (a == e)
+        if not ok.all():
+            bad[k] = int((~ok).sum())
+    print('parity', n, 'px', 'all fields' if fields is None else 'labels only',
+          'OK' if not bad else bad)
