@@ -53,8 +53,12 @@ __device__ inline void defer_append(bool deferred, int64_t p, int lane, int64_t*
 }
 
 // Stage 1 (wave-lockstep body, lt_fast.h): one wave per workgroup, the pixel series in LDS.
+// Occupancy target: 4 waves per SIMD (<= 128 VGPRs) where the body fits without spilling.
+#ifndef LT_FAST_WAVES_BIG
+#define LT_FAST_WAVES_BIG 4
+#endif
 template <int MAXY, int RMAX>
-__global__ __launch_bounds__(64, 4) void analyze_fast_kernel(const lt::DevScene* __restrict__ S,
+__global__ __launch_bounds__(64, (MAXY <= 32 && RMAX == 1) ? 4 : LT_FAST_WAVES_BIG) void analyze_fast_kernel(const lt::DevScene* __restrict__ S,
                                                           const lt_params P, const lt_tile_in in,
                                                           const lt_tile_out out,
                                                           const lt::lsq_xf* __restrict__ xtab,
@@ -362,9 +366,9 @@ int lt_analyze_tile(lt_ctx* c, const lt_scene* sc, const lt_params* prm, const l
 #define LT_LAUNCH_FAST(MY, RM)                                                              \
   hipLaunchKernelGGL((analyze_fast_kernel<MY, RM>), fgrid, fblock, 0, stream, c->d_scene, *prm, \
                      *in, *out, c->d_xtab, c->d_defer, c->d_ndefer)
-#ifdef LT_DEV_ONE_CONFIG  // assembly-inspection builds only (-S): the c2 instances alone
-  (void)one; (void)few;
-  LT_LAUNCH_FAST(32, 1);
+#ifdef LT_DEV_ONE_CONFIG  // A/B and assembly builds only: the (MAXY = LT_DEV_ONE_CONFIG, 1 rule)
+  (void)one; (void)few;     // instances alone
+  LT_LAUNCH_FAST(LT_DEV_ONE_CONFIG, 1);
 #else
   if (Y <= 32) {
     if (one) LT_LAUNCH_FAST(32, 1); else if (few) LT_LAUNCH_FAST(32, 4); else LT_LAUNCH_FAST(32, 16);
@@ -391,7 +395,7 @@ int lt_analyze_tile(lt_ctx* c, const lt_scene* sc, const lt_params* prm, const l
     LT_LAUNCH_RESOLVE1(MY, RM, double, c->d_defer + in->n_pix, c->d_ndefer + 2);            \
   } while (0)
 #ifdef LT_DEV_ONE_CONFIG
-  LT_LAUNCH_RESOLVE(32, 1);
+  LT_LAUNCH_RESOLVE(LT_DEV_ONE_CONFIG, 1);
 #else
   if (Y <= 32) {
     if (one) LT_LAUNCH_RESOLVE(32, 1); else if (few) LT_LAUNCH_RESOLVE(32, 4); else LT_LAUNCH_RESOLVE(32, 16);

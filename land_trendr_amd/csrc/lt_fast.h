@@ -13,9 +13,18 @@
 #pragma once
 #include "lt_pixel.h"
 
-// Diagnostic builds only (never the product): LT_ABLATE=1 skips the vertex fits, 2 the DP.
+// Diagnostic builds only (never the product): LT_ABLATE=1 skips the vertex fits, 2 the DP,
+// 3 the DP and despike's two sums, 4 the DP and the whole despike stage.
 #ifndef LT_ABLATE
 #define LT_ABLATE 0
+#endif
+// winner-pick batch: year slots whose value loads are issued together
+#ifndef LT_WB
+#define LT_WB 8
+#endif
+// the exact DP keeps OPT in private memory up to this many years, in registers above
+#ifndef LT_RESOLVE_PRIV_MAXY
+#define LT_RESOLVE_PRIV_MAXY 32
 #endif
 
 namespace lt {
@@ -89,7 +98,7 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
   bool f32_bad = false;
   // years in batches of 8: the winners first, then their 8 value loads issued together (one
   // load per year in sequence would leave each wave waiting out the HBM latency 30 times)
-  constexpr int WB = 8;
+  constexpr int WB = LT_WB;
   for (int yb = 0; yb < Y; yb += WB) {
     int best[WB];
 #pragma unroll
@@ -180,30 +189,40 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
     const int n8 = (ok && T >= 8) ? T - (T % 8) : 0;
     const int n8max = wave_max(n8);
     const int n8min = -wave_max(-n8);
+    // elements are read eight at a time (eight LDS reads in flight, then the adds)
     auto npsum = [&](auto term) {
       double r0 = 0.0, r1 = 0.0, r2 = 0.0, r3 = 0.0, r4 = 0.0, r5 = 0.0, r6 = 0.0, r7 = 0.0;
-      for (int t = 0; t < n8max; t++) {
-        const bool in = t < n8;
-        const double a = in ? term(t) : 0.0;
-        switch (t & 7) {  // wave-uniform
-          case 0: r0 = !in ? r0 : t < 8 ? a : r0 + a; break;
-          case 1: r1 = !in ? r1 : t < 8 ? a : r1 + a; break;
-          case 2: r2 = !in ? r2 : t < 8 ? a : r2 + a; break;
-          case 3: r3 = !in ? r3 : t < 8 ? a : r3 + a; break;
-          case 4: r4 = !in ? r4 : t < 8 ? a : r4 + a; break;
-          case 5: r5 = !in ? r5 : t < 8 ? a : r5 + a; break;
-          case 6: r6 = !in ? r6 : t < 8 ? a : r6 + a; break;
-          default: r7 = !in ? r7 : t < 8 ? a : r7 + a; break;
+      for (int t0 = 0; t0 < n8max; t0 += 8) {  // t0 wave-uniform, t0 + 7 < n8max <= MAXY
+        const bool in = t0 < n8;
+        double a[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) a[u] = term(t0 + u);
+        if (t0 == 0) {  // r_k starts as element k
+          r0 = a[0]; r1 = a[1]; r2 = a[2]; r3 = a[3];
+          r4 = a[4]; r5 = a[5]; r6 = a[6]; r7 = a[7];
+        } else if (in) {
+          r0 = r0 + a[0]; r1 = r1 + a[1]; r2 = r2 + a[2]; r3 = r3 + a[3];
+          r4 = r4 + a[4]; r5 = r5 + a[5]; r6 = r6 + a[6]; r7 = r7 + a[7];
         }
       }
       double seq = n8 > 0 ? ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)) : 0.0;
-      for (int t = n8min; t < Tmax; t++) {
-        if (ok && t >= n8 && t < T) seq += term(t);
+      for (int t0 = n8min; t0 < Tmax; t0 += 8) {
+        double a[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) a[u] = t0 + u < Tmax ? term(t0 + u) : 0.0;  // uniform guard
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          const int t = t0 + u;
+          if (ok && t >= n8 && t < T) seq += a[u];  // sequential, in element order
+        }
       }
       return seq;
     };
-    const double avg = npsum([&](int t) { return L.ys[t][lane]; }) / (double)T;
-    const double sd = __builtin_sqrt(npsum([&](int t) {
+    if constexpr (LT_ABLATE == 4) {
+      n = ok ? T : 0;
+    } else {
+    const double avg = LT_ABLATE == 3 ? 0.0 : npsum([&](int t) { return L.ys[t][lane]; }) / (double)T;
+    const double sd = LT_ABLATE == 3 ? __builtin_inf() : __builtin_sqrt(npsum([&](int t) {
                                        const double d = avg - L.ys[t][lane];
                                        return d * d;
                                      }) /
@@ -219,27 +238,39 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
       L.xn[0][lane] = (uint8_t)(L.year[y] - y0);
       n = 1;
     }
-    for (int t = 1; t < Tmax; t++) {
-      if (!(ok && t < T)) continue;
-      bool is_spike = false;
-      if (t + 1 < T) {  // the last point is never a spike
-        const double zv = L.ys[t + 1][lane];
-        const bool mono = (xv <= yv && yv <= zv) || (xv >= yv && yv >= zv);
-        is_spike = !mono && (__builtin_fabs(yv - xv) > sd && __builtin_fabs(yv - zv) > sd) &&
-                   yv != last_good;
-        if (!is_spike) last_good = yv;
-        xv = yv;
-        yv = zv;
+    for (int t0 = 1; t0 < Tmax; t0 += 8) {
+      // the next eight right neighbours first (eight LDS reads in flight); this block's writes
+      // go to slots <= t0 + 7, all read already
+      double z[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) z[u] = t0 + u + 1 < Tmax ? (double)L.ys[t0 + u + 1][lane] : 0.0;
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const int t = t0 + u;
+        if (t >= Tmax) break;  // wave-uniform
+        if (!(ok && t < T)) continue;
+        const double cur = yv;  // ys[t]
+        bool is_spike = false;
+        if (t + 1 < T) {  // the last point is never a spike
+          const double zv = z[u];
+          const bool mono = (xv <= yv && yv <= zv) || (xv >= yv && yv >= zv);
+          is_spike = !mono && (__builtin_fabs(yv - xv) > sd && __builtin_fabs(yv - zv) > sd) &&
+                     yv != last_good;
+          if (!is_spike) last_good = yv;
+          xv = yv;
+          yv = zv;
+        }
+        const int y = __builtin_ctzll(rem);
+        rem &= rem - 1;
+        if (is_spike) {
+          spike |= 1ull << t;
+          continue;
+        }
+        if (n != t) L.ys[n][lane] = (VT)cur;
+        L.xn[n][lane] = (uint8_t)(L.year[y] - y0);
+        n++;
       }
-      const int y = __builtin_ctzll(rem);
-      rem &= rem - 1;
-      if (is_spike) {
-        spike |= 1ull << t;
-        continue;
-      }
-      if (n != t) L.ys[n][lane] = L.ys[t][lane];
-      L.xn[n][lane] = (uint8_t)(L.year[y] - y0);
-      n++;
+    }
     }
   }
   const int nmax = wave_max(n);
@@ -259,7 +290,7 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
     else return AG[j];
   };
   if constexpr (EXACT) {
-    if constexpr (MAXY <= 32) {
+    if constexpr (MAXY <= LT_RESOLVE_PRIV_MAXY) {
       // ---- exact-OPT DP: closed-form intervals, then the emulated LAPACK residual for every
       // start whose interval reaches the column's smallest upper bound; first exact minimum ----
       const double c = P.line_cost;
@@ -457,7 +488,7 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
         j = a - 1;
       }
     }
-  } else if (nmax >= 1 && LT_ABLATE != 2) {
+  } else if (nmax >= 1 && LT_ABLATE < 2) {
     const double c = P.line_cost;
     const double inf = __builtin_inf();
     double OPTa[MAXY + 1];  // per-lane private memory (wave-uniform indices)

@@ -16,9 +16,11 @@ from land_trendr_amd.synth import make_scene  # noqa: E402
 from oracle import oracle  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 17
-sc = make_scene(n, n_years=30, seed=int(sys.argv[2]) if len(sys.argv) > 2 else 11)
+years = int(sys.argv[3]) if len(sys.argv) > 3 else 30
+lc = float(sys.argv[4]) if len(sys.argv) > 4 else 10.0
+sc = make_scene(n, n_years=years, seed=int(sys.argv[2]) if len(sys.argv) > 2 else 11)
 meta = build_scene(sc.dates, parse_date('2014-07-01'))
-params, _ = compile_params(10.0, [{'name': 'gd', 'val': 1, 'change_type': 'GD'}])
+params, _ = compile_params(lc, [{'name': 'gd', 'val': 1, 'change_type': 'GD'}])
 eng = get_engine(0)
 exp = oracle.analyze_tile(meta, params, sc.values.numpy(), None, n_threads=16)
 for fields in (None, ('status', 'n_years', 'matched', 'class_val', 'onset_year', 'duration',
