@@ -80,6 +80,22 @@ def pmc_traffic(kernel, px_per_launch, input_mode):
         return None
 
 
+def pmc_fp64_issued(kernel, px_per_launch, input_mode):
+    """FP64 flops the hardware issued per launch of `kernel` (PMC SQ_INSTS_VALU_{ADD,MUL,FMA}_F64
+    x 64 lanes, FMA = 2) from the committed summary, scaled to this launch's pixel count."""
+    try:
+        with open(PMC_SUMMARY) as f:
+            d = json.load(f)
+        if d.get('_input', 'index') != input_mode:
+            return None
+        k = d[kernel]
+        wave_flops = (k['SQ_INSTS_VALU_ADD_F64'] + k['SQ_INSTS_VALU_MUL_F64'] +
+                      2 * k['SQ_INSTS_VALU_FMA_F64'])
+        return 64 * wave_flops / d['_pixels_per_launch'] * px_per_launch
+    except (OSError, KeyError, ValueError, TypeError, ZeroDivisionError):
+        return None
+
+
 def cpu_baseline(cfg, seconds):
     """The oracle (C restatement, pthreads over all host cores) on a bounded sample."""
     from oracle import oracle
@@ -245,6 +261,8 @@ def main():
                 if idx_events else None)
     hbm_gbs = bpp * px_per_launch / (kern_ms * 1e-3) / 1e9
     traffic = pmc_traffic('analyze', px_per_launch, args.input) if args.config == 'c2' else None
+    issued = (pmc_fp64_issued('analyze', px_per_launch, args.input) if args.config == 'c2'
+              else None)
     res = {
         'metric': 'Mpixels/sec full analyze (30-yr series)' if cfg['years'] == 30 else
                   'Mpixels/sec full analyze (%d-yr series)' % cfg['years'],
@@ -271,7 +289,14 @@ def main():
                      'flops_per_px': f_ref(cfg['years']), 'flops_model': 'F_ref (SURVEY.md 8(d))',
                      'algorithmic_bytes_per_px': bpp,
                      'hbm': {'achieved': round(hbm_gbs, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                             'frac': round(hbm_gbs / HBM_PEAK_GBS, 4)}},
+                             'frac': round(hbm_gbs / HBM_PEAK_GBS, 4)},
+                     # what the hardware executed: FP64 VALU flops from the PMC summary / this
+                     # launch's time (the DP's integer, compare and select work is not counted)
+                     'fp64_issued': None if issued is None else {
+                         'achieved': round(issued / (kern_ms * 1e-3) / 1e12, 3),
+                         'peak': FP64_PEAK_TFLOPS, 'unit': 'TFLOP/s',
+                         'frac': round(issued / (kern_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS, 4),
+                         'source': os.path.relpath(PMC_SUMMARY, ROOT)}},
         'status_numeric_pixels': n_numeric,
         'load_stage': None if index_ms is None else {
             'kernel': 'lt_index_kernel (hiprtc, index_eqn "B1 - B2", int16 bands -> int16)',
