@@ -18,6 +18,9 @@
 #ifndef LT_ABLATE
 #define LT_ABLATE 0
 #endif
+#ifndef LT_SAMEKEY  // timing experiment only: every 2-point fit reads table slot 0 (wrong results)
+#define LT_SAMEKEY 0
+#endif
 // winner-pick batch: year slots whose value loads are issued together
 #ifndef LT_WB
 #define LT_WB 8
@@ -48,7 +51,7 @@ template <class GX, class GY>
 __device__ inline int lsq_lockstep(bool act, int m, GX X, GY Y, const lsq_xf* __restrict__ xtab,
                                    bool need_solution, bool need_ssr, double& slope, double& icpt,
                                    double& ssr) {
-  const int key = act ? xset_key(m, X) : 0;
+  const int key = act ? (LT_SAMEKEY && m == 2 ? 0 : xset_key(m, X)) : 0;
   const bool miss = act && key < 0;
   lsq_xf f;
   if (act && !miss) f = xtab[key];
@@ -497,15 +500,19 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
     double Emax = 0.0;       // bound on |OPTa[k] - OPT[k]| for every inexact k so far
     // register window of the four most recent points (x, y of points j..j-3) and of OPTa[j..j-3]:
     // the 1- to 4-point starts of a column, nearly all the DP prices, read no LDS or private
-    // memory
-    double opt_j = 0.0, opt_jm1 = 0.0, opt_jm2 = 0.0, opt_jm3 = 0.0;
-    int wx0 = 0, wx1 = 0, wx2 = 0, wx3 = 0;
-    double wy0 = 0.0, wy1 = 0.0, wy2 = 0.0, wy3 = 0.0;
+    // memory. Four register slots per quantity; the column loop is unrolled by four and each
+    // column receives the slots rotated, so the window moves without register copies.
+    int xA = 0, xB = 0, xC = 0, xD = 0;
+    double yA = 0.0, yB = 0.0, yC = 0.0, yD = 0.0;
+    double oA = 0.0, oB = 0.0, oC = 0.0, oD = 0.0;  // oA = OPTa[0] for column 0
     double SyyAll = 0.0;                // sum of y^2 over the points 0..j
     const bool prune = c >= 0.0;
     uint64_t amb = 0;
-    for (int jj = 0; jj < nmax; jj++) {
-      const int j = __builtin_amdgcn_readfirstlane(jj);  // column index in an SGPR
+    // column j: wx0 receives point j (its slot held point j-4); wx1..wx3 hold points j-1..j-3;
+    // opt_j..opt_jm3 hold OPTa[j..j-3], and OPTa[j+1] is written over opt_jm3
+    auto column = [&](const int j, int& wx0, int& wx1, int& wx2, int& wx3, double& wy0,
+                      double& wy1, double& wy2, double& wy3, double& opt_j, double& opt_jm1,
+                      double& opt_jm2, double& opt_jm3) __attribute__((always_inline)) {
       const bool col = j < n;
       double Sy = 0.0, Sxy = 0.0, Syy = 0.0;
       int Sx = 0, Sxx = 0;
@@ -541,13 +548,7 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
         }
       }
       // prefix bound for the early exit below: every segment ending at j has Syy <= SyyAll
-      wx3 = wx2;
-      wx2 = wx1;
-      wx1 = wx0;
       wx0 = L.xn[j][lane];
-      wy3 = wy2;
-      wy2 = wy1;
-      wy1 = wy0;
       wy0 = (double)L.ys[j][lane];
       SyyAll = __builtin_fma(wy0, wy0, SyyAll);
       auto add_xy = [&](int xi, double yi) {
@@ -658,11 +659,15 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
         OPTa[j + 1] = vnew;  // wave-uniform index
         if (exnew) exact |= 2ull << j;
         Emax = enew > Emax ? enew : Emax;
-        opt_jm3 = opt_jm2;
-        opt_jm2 = opt_jm1;
-        opt_jm1 = opt_j;
-        opt_j = vnew;
+        opt_jm3 = vnew;  // OPTa[j+1]: the slot of OPTa[j-3], which no later column reads
       }
+    };
+    for (int jj = 0; jj < nmax; jj += 4) {
+      const int j = __builtin_amdgcn_readfirstlane(jj);  // column index in an SGPR
+      column(j, xA, xB, xC, xD, yA, yB, yC, yD, oA, oB, oC, oD);
+      if (j + 1 < nmax) column(j + 1, xD, xA, xB, xC, yD, yA, yB, yC, oD, oA, oB, oC);
+      if (j + 2 < nmax) column(j + 2, xC, xD, xA, xB, yC, yD, yA, yB, oC, oD, oA, oB);
+      if (j + 3 < nmax) column(j + 3, xB, xC, xD, xA, yB, yC, yD, yA, oB, oC, oD, oA);
     }
     // find_segments (utils.py:633-644): starts of the optimal segments + the last point
     if (n >= 1) {
