@@ -193,31 +193,43 @@ def main():
                 for f in LABEL_GATHER_FIELDS}
     works = []
 
+    # tiles per lt_analyze_tiles call: all of them, or groups whose label rasters go to RCCL
+    # while the next group computes
+    group = len(tiles) if not gather else 4
+
     def step(timed=False):
-        for t, (p0, p1) in enumerate(tiles):
-            view = {f: x[..., :p1 - p0] for f, x in slabs[t].items()}
+        values = []
+        for t, (p0, p1) in enumerate(tiles):  # the load stage: index_eqn over every tile
             if bands_in:
                 e0 = e1 = None
                 if timed:
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(
                         enable_timing=True)
                     e0.record()
-                values = eng.index_tile(index_fn, sc.bands[:, :, p0:p1],
-                                        out=index_buf[:, p0:p1])
+                values.append(eng.index_tile(index_fn, sc.bands[:, :, p0:p1],
+                                             out=index_buf[:, p0:p1]))
                 if timed:
                     e1.record()
                     idx_events.append((e0, e1))
             else:
-                values = sc.values[:, p0:p1]
-            eng.analyze_tile(meta, params, values,
-                             sc.valid[:, p0:p1] if sc.valid is not None else None,
-                             fields, out=view)
-            if gather:  # this tile's label rasters to the writer rank, on
-                # RCCL's stream: it runs while the next tiles compute
-                for f in LABEL_GATHER_FIELDS:
-                    works.append(dist.gather(
-                        slabs[t][f], [recv[f][r][t] for r in range(world)] if rank == 0 else None,
-                        dst=0, async_op=True))
+                values.append(sc.values[:, p0:p1])
+        for g0 in range(0, len(tiles), group):
+            ts = range(g0, min(len(tiles), g0 + group))
+            # analyze + label (tile t's resolve stage beside tile t+1's analyze stage)
+            eng.analyze_tiles(
+                meta, params,
+                [(values[t], sc.valid[:, tiles[t][0]:tiles[t][1]] if sc.valid is not None
+                  else None) for t in ts], fields,
+                outs=[{f: x[..., :tiles[t][1] - tiles[t][0]] for f, x in slabs[t].items()}
+                      for t in ts])
+            if gather:  # these tiles' label rasters to the writer rank, on
+                # RCCL's stream: they travel while the next group computes
+                for t in ts:
+                    for f in LABEL_GATHER_FIELDS:
+                        works.append(dist.gather(
+                            slabs[t][f],
+                            [recv[f][r][t] for r in range(world)] if rank == 0 else None,
+                            dst=0, async_op=True))
         while works:
             works.pop().wait()
 

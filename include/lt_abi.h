@@ -193,6 +193,14 @@ const char* lt_last_error(const lt_ctx* ctx);
 int lt_analyze_tile(lt_ctx* ctx, const lt_scene* scene, const lt_params* params,
                     const lt_tile_in* in, const lt_tile_out* out, void* stream);
 
+/* lt_analyze_tile over n_tiles tiles of one scene (the reducer loop over a batch of grid-point
+ * tiles, mr_land_trendr_job.py:83-126). Tile t's resolve kernels run on the context's own side
+ * stream beside tile t+1's analyze kernel; every output is complete in `stream` order once the
+ * call's work is done (`stream` waits for the last resolve). Same results as n_tiles calls of
+ * lt_analyze_tile. */
+int lt_analyze_tiles(lt_ctx* ctx, const lt_scene* scene, const lt_params* params, int n_tiles,
+                     const lt_tile_in* ins, const lt_tile_out* outs, void* stream);
+
 /* change_labeling alone (utils.py:795-820) on trendlines already in device memory. Writes the
  * rule planes of `out` and out->status (only LT_ST_PRE_THRESHOLD_ATTR can be set). */
 int lt_label_tile(lt_ctx* ctx, const lt_label_in* in, const lt_params* params,

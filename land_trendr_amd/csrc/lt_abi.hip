@@ -180,6 +180,11 @@ struct lt_ctx {
   unsigned long long* d_ndefer = nullptr;
   int64_t defer_cap = 0;
   lt::lsq_xf* d_xtab = nullptr;  // x-set factor table (built at context creation)
+  hipStream_t side = nullptr;    // the resolve stage's stream (lt_analyze_tiles)
+  hipEvent_t ev_analyzed[2] = {nullptr, nullptr};  // per deferred-list set
+  hipEvent_t ev_resolved[2] = {nullptr, nullptr};
+  bool set_used[2] = {false, false};
+  int last_set = 0;
   std::map<std::string, lt_index*> index_fns;  // compiled load-stage kernels, by source
 };
 
@@ -238,6 +243,14 @@ int lt_ctx_destroy(lt_ctx* c) {
     (void)hipEventDestroy(ep.start);
     (void)hipEventDestroy(ep.stop);
   }
+  if (c->side) {
+    (void)hipStreamSynchronize(c->side);
+    (void)hipStreamDestroy(c->side);
+  }
+  for (int s = 0; s < 2; s++) {
+    if (c->ev_analyzed[s]) (void)hipEventDestroy(c->ev_analyzed[s]);
+    if (c->ev_resolved[s]) (void)hipEventDestroy(c->ev_resolved[s]);
+  }
   if (c->d_defer) (void)hipFree(c->d_defer);
   if (c->d_ndefer) (void)hipFree(c->d_ndefer);
   if (c->d_scene) (void)hipFree(c->d_scene);
@@ -276,16 +289,112 @@ int lt_ctx_stage_ms(lt_ctx* c, double* ms_out, int n_stages, int64_t* n_launches
   return LT_OK;
 }
 
-int lt_analyze_tile(lt_ctx* c, const lt_scene* sc, const lt_params* prm, const lt_tile_in* in,
-                    const lt_tile_out* out, void* stream_) {
-  if (!c) return LT_ERR_ARG;
-  if (!sc || !prm || !in || !out) return fail(c, LT_ERR_ARG, "null argument%s");
+static int check_tile(lt_ctx* c, const lt_tile_in* in, const lt_tile_out* out) {
+  if (!in || !out) return fail(c, LT_ERR_ARG, "null argument%s");
   if (in->n_pix < 0 || in->stride < in->n_pix || out->stride < in->n_pix)
     return fail(c, LT_ERR_ARG, "bad n_pix/stride%s");
-  if (in->n_pix == 0) return LT_OK;
+  if (in->n_pix == 0) return LT_OK;  // nothing is read or written
   if (!in->obs_val && !in->obs_index) return fail(c, LT_ERR_ARG, "obs_val or obs_index required%s");
   if (in->obs_index && !lt_idx::ctype(in->index_type))
     return fail(c, LT_ERR_ARG, "bad index_type%s");
+  return LT_OK;
+}
+
+// One tile's stages: the analyze kernel on `stream`, the resolve kernels (its deferred pixels) on
+// `rstream` once the analyze kernel is done; deferred-pixel list / counters set `set`.
+static int launch_tile(lt_ctx* c, const lt_params* prm, const lt_tile_in* in,
+                       const lt_tile_out* out, int Y, hipStream_t stream, hipStream_t rstream,
+                       int set) {
+  int64_t* dl = c->d_defer + (size_t)set * 2 * c->defer_cap;
+  unsigned long long* dn = c->d_ndefer + 4 * set;
+  // [0]/[2]: deferred-pixel counts of the binary32 / binary64 lists (stage 1), [1]/[3]: the
+  // resolve launches' work counters
+  HIP_OR_FAIL(c, hipMemsetAsync(dn, 0, 4 * sizeof(unsigned long long), stream));
+  EventPair* ep[2] = {nullptr, nullptr};
+  if (c->timing) {
+    while (c->pool.size() < c->used + 2) {  // grow first: pointers into the pool stay valid
+      EventPair np;
+      HIP_OR_FAIL(c, hipEventCreate(&np.start));
+      HIP_OR_FAIL(c, hipEventCreate(&np.stop));
+      c->pool.push_back(np);
+    }
+    ep[0] = &c->pool[c->used++];
+    ep[1] = &c->pool[c->used++];
+  }
+  if (ep[0]) HIP_OR_FAIL(c, hipEventRecord(ep[0]->start, stream));
+  const int64_t nwave = (in->n_pix + 63) / 64;
+  if (nwave > 0x7fffffff) return fail(c, LT_ERR_LIMIT, "tile too large%s");
+  dim3 fgrid((unsigned)nwave), fblock(64);
+  const bool one = prm->n_rules <= 1, few = prm->n_rules <= 4;
+#define LT_LAUNCH_FAST(MY, RM)                                                              \
+  hipLaunchKernelGGL((analyze_fast_kernel<MY, RM>), fgrid, fblock, 0, stream, c->d_scene, *prm, \
+                     *in, *out, c->d_xtab, dl, dn)
+#ifdef LT_DEV_ONE_CONFIG  // A/B and assembly builds only: the (MAXY = LT_DEV_ONE_CONFIG, 1 rule)
+  (void)one; (void)few;     // instances alone
+  LT_LAUNCH_FAST(LT_DEV_ONE_CONFIG, 1);
+#else
+  if (Y <= 32) {
+    if (one) LT_LAUNCH_FAST(32, 1); else if (few) LT_LAUNCH_FAST(32, 4); else LT_LAUNCH_FAST(32, 16);
+  } else if (Y <= 48) {
+    if (one) LT_LAUNCH_FAST(48, 1); else if (few) LT_LAUNCH_FAST(48, 4); else LT_LAUNCH_FAST(48, 16);
+  } else {
+    if (one) LT_LAUNCH_FAST(64, 1); else if (few) LT_LAUNCH_FAST(64, 4); else LT_LAUNCH_FAST(64, 16);
+  }
+#endif
+#undef LT_LAUNCH_FAST
+  HIP_OR_FAIL(c, hipGetLastError());
+  if (ep[0]) HIP_OR_FAIL(c, hipEventRecord(ep[0]->stop, stream));
+  if (rstream != stream) {
+    HIP_OR_FAIL(c, hipEventRecord(c->ev_analyzed[set], stream));
+    HIP_OR_FAIL(c, hipStreamWaitEvent(rstream, c->ev_analyzed[set], 0));
+  }
+  if (ep[1]) HIP_OR_FAIL(c, hipEventRecord(ep[1]->start, rstream));
+  stream = rstream;  // the resolve launches below
+#define LT_LAUNCH_RESOLVE1(MY, RM, VT, LIST, CNT)                                            \
+  do {                                                                                      \
+    const unsigned g = resolve_grid<MY, RM, VT>(c->device);                                 \
+    dim3 rg((unsigned)(nwave < (int64_t)g ? nwave : (int64_t)g));                           \
+    hipLaunchKernelGGL((resolve_fast_kernel<MY, RM, VT>), rg, fblock, 0, stream, c->d_scene, \
+                       *prm, *in, *out, c->d_xtab, LIST, CNT);                              \
+  } while (0)
+#define LT_LAUNCH_RESOLVE(MY, RM)                                                            \
+  do {                                                                                      \
+    LT_LAUNCH_RESOLVE1(MY, RM, float, dl, dn);                             \
+    LT_LAUNCH_RESOLVE1(MY, RM, double, dl + in->n_pix, dn + 2);            \
+  } while (0)
+#ifdef LT_DEV_ONE_CONFIG
+  LT_LAUNCH_RESOLVE(LT_DEV_ONE_CONFIG, 1);
+#else
+  if (Y <= 32) {
+    if (one) LT_LAUNCH_RESOLVE(32, 1); else if (few) LT_LAUNCH_RESOLVE(32, 4); else LT_LAUNCH_RESOLVE(32, 16);
+  } else if (Y <= 48) {
+    if (one) LT_LAUNCH_RESOLVE(48, 1); else if (few) LT_LAUNCH_RESOLVE(48, 4); else LT_LAUNCH_RESOLVE(48, 16);
+  } else {
+    if (one) LT_LAUNCH_RESOLVE(64, 1); else if (few) LT_LAUNCH_RESOLVE(64, 4); else LT_LAUNCH_RESOLVE(64, 16);
+  }
+#endif
+#undef LT_LAUNCH_RESOLVE
+#undef LT_LAUNCH_RESOLVE1
+  HIP_OR_FAIL(c, hipGetLastError());
+  if (ep[1]) HIP_OR_FAIL(c, hipEventRecord(ep[1]->stop, rstream));
+  HIP_OR_FAIL(c, hipEventRecord(c->ev_resolved[set], rstream));
+  c->last_set = set;
+  c->launches++;
+  return LT_OK;
+}
+
+int lt_analyze_tiles(lt_ctx* c, const lt_scene* sc, const lt_params* prm, int n_tiles,
+                     const lt_tile_in* ins, const lt_tile_out* outs, void* stream_) {
+  if (!c) return LT_ERR_ARG;
+  if (!sc || !prm || n_tiles < 0 || (n_tiles > 0 && (!ins || !outs)))
+    return fail(c, LT_ERR_ARG, "null argument%s");
+  int64_t cap = 0;
+  for (int t = 0; t < n_tiles; t++) {
+    const int rc = check_tile(c, &ins[t], &outs[t]);
+    if (rc != LT_OK) return rc;
+    cap = ins[t].n_pix > cap ? ins[t].n_pix : cap;
+  }
+  if (cap == 0) return LT_OK;
   const int K = sc->n_obs, Y = sc->n_years;
   if (K < 0 || K > LT_MAX_OBS || Y < 0 || Y > LT_MAX_YEARS)
     return fail(c, LT_ERR_LIMIT, "scene exceeds LT_MAX_OBS/LT_MAX_YEARS%s");
@@ -334,83 +443,46 @@ int lt_analyze_tile(lt_ctx* c, const lt_scene* sc, const lt_params* prm, const l
     c->scene_valid = true;
   }
 
-  // deferred-pixel list (grown on demand; sized for the largest tile seen)
-  if (c->defer_cap < in->n_pix) {
+  // deferred-pixel lists: two sets (tile t uses set t % 2), sized for the largest tile seen
+  if (c->defer_cap < cap) {
+    // a smaller list may still be read by an earlier call's resolve on the side stream
+    if (c->side) HIP_OR_FAIL(c, hipStreamSynchronize(c->side));
     if (c->d_defer) HIP_OR_FAIL(c, hipFree(c->d_defer));
     c->d_defer = nullptr;
-    HIP_OR_FAIL(c, hipMalloc((void**)&c->d_defer, 2 * sizeof(int64_t) * (size_t)in->n_pix));
+    HIP_OR_FAIL(c, hipMalloc((void**)&c->d_defer, 2 * 2 * sizeof(int64_t) * (size_t)cap));
     if (!c->d_ndefer)
-      HIP_OR_FAIL(c, hipMalloc((void**)&c->d_ndefer, 4 * sizeof(unsigned long long)));
-    c->defer_cap = in->n_pix;
+      HIP_OR_FAIL(c, hipMalloc((void**)&c->d_ndefer, 2 * 4 * sizeof(unsigned long long)));
+    c->defer_cap = cap;
   }
-  // [0]/[2]: deferred-pixel counts of the binary32 / binary64 lists (stage 1), [1]/[3]: the
-  // resolve launches' work counters
-  HIP_OR_FAIL(c, hipMemsetAsync(c->d_ndefer, 0, 4 * sizeof(unsigned long long), stream));
-
-  EventPair* ep[2] = {nullptr, nullptr};
-  if (c->timing) {
-    while (c->pool.size() < c->used + 2) {  // grow first: pointers into the pool stay valid
-      EventPair np;
-      HIP_OR_FAIL(c, hipEventCreate(&np.start));
-      HIP_OR_FAIL(c, hipEventCreate(&np.stop));
-      c->pool.push_back(np);
+  if (!c->side) {
+    HIP_OR_FAIL(c, hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+    for (int s = 0; s < 2; s++) {
+      HIP_OR_FAIL(c, hipEventCreateWithFlags(&c->ev_analyzed[s], hipEventDisableTiming));
+      HIP_OR_FAIL(c, hipEventCreateWithFlags(&c->ev_resolved[s], hipEventDisableTiming));
     }
-    ep[0] = &c->pool[c->used++];
-    ep[1] = &c->pool[c->used++];
   }
-  if (ep[0]) HIP_OR_FAIL(c, hipEventRecord(ep[0]->start, stream));
-  const int64_t nwave = (in->n_pix + 63) / 64;
-  if (nwave > 0x7fffffff) return fail(c, LT_ERR_LIMIT, "tile too large%s");
-  dim3 fgrid((unsigned)nwave), fblock(64);
-  const bool one = prm->n_rules <= 1, few = prm->n_rules <= 4;
-#define LT_LAUNCH_FAST(MY, RM)                                                              \
-  hipLaunchKernelGGL((analyze_fast_kernel<MY, RM>), fgrid, fblock, 0, stream, c->d_scene, *prm, \
-                     *in, *out, c->d_xtab, c->d_defer, c->d_ndefer)
-#ifdef LT_DEV_ONE_CONFIG  // A/B and assembly builds only: the (MAXY = LT_DEV_ONE_CONFIG, 1 rule)
-  (void)one; (void)few;     // instances alone
-  LT_LAUNCH_FAST(LT_DEV_ONE_CONFIG, 1);
-#else
-  if (Y <= 32) {
-    if (one) LT_LAUNCH_FAST(32, 1); else if (few) LT_LAUNCH_FAST(32, 4); else LT_LAUNCH_FAST(32, 16);
-  } else if (Y <= 48) {
-    if (one) LT_LAUNCH_FAST(48, 1); else if (few) LT_LAUNCH_FAST(48, 4); else LT_LAUNCH_FAST(48, 16);
-  } else {
-    if (one) LT_LAUNCH_FAST(64, 1); else if (few) LT_LAUNCH_FAST(64, 4); else LT_LAUNCH_FAST(64, 16);
+  // Tile t: analyze on `stream`, resolve on the context's side stream, so tile t's resolve runs
+  // beside tile t+1's analyze (the resolve is a few long waves: latency, not throughput). Set
+  // t % 2 is reused by tile t+2 only after tile t's resolve; at the end `stream` waits for the
+  // last resolve, so every output is complete in `stream` order when the call's work is done.
+  for (int t = 0; t < n_tiles; t++) {
+    if (ins[t].n_pix == 0) continue;
+    const int set = t & 1;
+    if (c->set_used[set]) HIP_OR_FAIL(c, hipStreamWaitEvent(stream, c->ev_resolved[set], 0));
+    const int rc = launch_tile(c, prm, &ins[t], &outs[t], Y, stream, c->side, set);
+    if (rc != LT_OK) return rc;
+    c->set_used[set] = true;
   }
-#endif
-#undef LT_LAUNCH_FAST
-  HIP_OR_FAIL(c, hipGetLastError());
-  if (ep[0]) HIP_OR_FAIL(c, hipEventRecord(ep[0]->stop, stream));
-  if (ep[1]) HIP_OR_FAIL(c, hipEventRecord(ep[1]->start, stream));
-#define LT_LAUNCH_RESOLVE1(MY, RM, VT, LIST, CNT)                                            \
-  do {                                                                                      \
-    const unsigned g = resolve_grid<MY, RM, VT>(c->device);                                 \
-    dim3 rg((unsigned)(nwave < (int64_t)g ? nwave : (int64_t)g));                           \
-    hipLaunchKernelGGL((resolve_fast_kernel<MY, RM, VT>), rg, fblock, 0, stream, c->d_scene, \
-                       *prm, *in, *out, c->d_xtab, LIST, CNT);                              \
-  } while (0)
-#define LT_LAUNCH_RESOLVE(MY, RM)                                                            \
-  do {                                                                                      \
-    LT_LAUNCH_RESOLVE1(MY, RM, float, c->d_defer, c->d_ndefer);                             \
-    LT_LAUNCH_RESOLVE1(MY, RM, double, c->d_defer + in->n_pix, c->d_ndefer + 2);            \
-  } while (0)
-#ifdef LT_DEV_ONE_CONFIG
-  LT_LAUNCH_RESOLVE(LT_DEV_ONE_CONFIG, 1);
-#else
-  if (Y <= 32) {
-    if (one) LT_LAUNCH_RESOLVE(32, 1); else if (few) LT_LAUNCH_RESOLVE(32, 4); else LT_LAUNCH_RESOLVE(32, 16);
-  } else if (Y <= 48) {
-    if (one) LT_LAUNCH_RESOLVE(48, 1); else if (few) LT_LAUNCH_RESOLVE(48, 4); else LT_LAUNCH_RESOLVE(48, 16);
-  } else {
-    if (one) LT_LAUNCH_RESOLVE(64, 1); else if (few) LT_LAUNCH_RESOLVE(64, 4); else LT_LAUNCH_RESOLVE(64, 16);
-  }
-#endif
-#undef LT_LAUNCH_RESOLVE
-#undef LT_LAUNCH_RESOLVE1
-  HIP_OR_FAIL(c, hipGetLastError());
-  if (ep[1]) HIP_OR_FAIL(c, hipEventRecord(ep[1]->stop, stream));
-  c->launches++;
+  HIP_OR_FAIL(c, hipEventRecord(c->ev_resolved[c->last_set], c->side));
+  HIP_OR_FAIL(c, hipStreamWaitEvent(stream, c->ev_resolved[c->last_set], 0));
   return LT_OK;
+}
+
+int lt_analyze_tile(lt_ctx* c, const lt_scene* sc, const lt_params* prm, const lt_tile_in* in,
+                    const lt_tile_out* out, void* stream_) {
+  if (!c) return LT_ERR_ARG;
+  if (!in || !out) return fail(c, LT_ERR_ARG, "null argument%s");
+  return lt_analyze_tiles(c, sc, prm, 1, in, out, stream_);
 }
 
 int lt_ctx_last_deferred(lt_ctx* c, int64_t* n_deferred) {
@@ -419,7 +491,8 @@ int lt_ctx_last_deferred(lt_ctx* c, int64_t* n_deferred) {
   if (!c->d_ndefer) return LT_OK;
   HIP_OR_FAIL(c, hipSetDevice(c->device));
   unsigned long long v[4] = {0, 0, 0, 0};
-  HIP_OR_FAIL(c, hipMemcpy(v, c->d_ndefer, sizeof v, hipMemcpyDeviceToHost));
+  HIP_OR_FAIL(c, hipDeviceSynchronize());  // the counters of the last tile's set
+  HIP_OR_FAIL(c, hipMemcpy(v, c->d_ndefer + 4 * c->last_set, sizeof v, hipMemcpyDeviceToHost));
   *n_deferred = (int64_t)(v[0] + v[2]);
   return LT_OK;
 }

@@ -76,6 +76,37 @@ class Engine:
         (int16, uint16, int32, float32, uint8, ...: what index_tile writes) — valid: uint8 [K, P]
         or None. Returns the dict of output tensors ([Y, P], [R, P], [P]); asynchronous on
         `stream`."""
+        tin, tout, out = self._tile_structs(scene, params, values, valid, fields, out)
+        sc = scene.to_c()
+        st = stream if stream is not None else torch.cuda.current_stream(self.device)
+        rc = self.lib.lt_analyze_tile(self.ctx, ctypes.byref(sc), ctypes.byref(params),
+                                      ctypes.byref(tin), ctypes.byref(tout),
+                                      ctypes.c_void_p(st.cuda_stream))
+        self._check(rc, 'lt_analyze_tile')
+        return out
+
+    def analyze_tiles(self, scene, params, tiles, fields=ALL_FIELDS, outs=None, stream=None):
+        """analyze_tile over a list of (values, valid) tiles of one scene in one call
+        (lt_analyze_tiles: tile t's resolve stage overlaps tile t+1's analyze stage). Returns the
+        list of output dicts; asynchronous on `stream`."""
+        n = len(tiles)
+        tins = (_abi.LtTileIn * max(n, 1))()
+        touts = (_abi.LtTileOut * max(n, 1))()
+        res = []
+        for t, (values, valid) in enumerate(tiles):
+            tin, tout, o = self._tile_structs(scene, params, values, valid, fields,
+                                              outs[t] if outs is not None else None)
+            tins[t] = tin
+            touts[t] = tout
+            res.append(o)
+        sc = scene.to_c()
+        st = stream if stream is not None else torch.cuda.current_stream(self.device)
+        rc = self.lib.lt_analyze_tiles(self.ctx, ctypes.byref(sc), ctypes.byref(params), n, tins,
+                                       touts, ctypes.c_void_p(st.cuda_stream))
+        self._check(rc, 'lt_analyze_tiles')
+        return res
+
+    def _tile_structs(self, scene, params, values, valid, fields, out):
         if values.dtype not in _LT_T or values.device != self.device or values.dim() != 2:
             raise LtError('values must be a [K, P] raster tensor on %s' % self.device)
         if values.stride(1) != 1:
@@ -116,13 +147,7 @@ class Engine:
         tout.stride = ostride if ostride is not None else P
         for f, t in out.items():
             setattr(tout, f, ctypes.cast(t.data_ptr(), type(getattr(tout, f))))
-        sc = scene.to_c()
-        st = stream if stream is not None else torch.cuda.current_stream(self.device)
-        rc = self.lib.lt_analyze_tile(self.ctx, ctypes.byref(sc), ctypes.byref(params),
-                                      ctypes.byref(tin), ctypes.byref(tout),
-                                      ctypes.c_void_p(st.cuda_stream))
-        self._check(rc, 'lt_analyze_tile')
-        return out
+        return tin, tout, out
 
     # --- load stage: index_eqn (rast_algebra, utils.py:447-484) ---
     def compile_index(self, program):
