@@ -137,6 +137,9 @@ def main():
                     help='N>1: skip the RCCL gather of label rasters to rank 0')
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--serial-load', action='store_true',
+                    help='run every tile\'s index_eqn kernel ahead of the analyze kernels on '
+                         'one stream (default: load stage on its own stream, per-tile events)')
     ap.add_argument('--input', default='bands', choices=['bands', 'index'],
                     help='bands: int16 B1, B2 planes + index_eqn "B1 - B2" on the GPU (the '
                          'reference pipeline, SURVEY.md 8(d)); index: float64 index values')
@@ -197,22 +200,37 @@ def main():
     # while the next group computes
     group = len(tiles) if not gather else 4
 
+    # the load stage runs on its own stream: tile t's analyze kernel waits only for tile t's
+    # index raster, so later tiles' index kernels (HBM-bound) run beside earlier tiles' analyze
+    # kernels (issue-bound) instead of all of them ahead of the first analyze
+    load_stream = torch.cuda.Stream(dev) if bands_in and not args.serial_load else None
+
     def step(timed=False):
-        values = []
+        values, ready = [], []
+        main = torch.cuda.current_stream(dev)
+        if load_stream is not None:  # the previous step's analyze kernels read index_buf
+            load_stream.wait_stream(main)
         for t, (p0, p1) in enumerate(tiles):  # the load stage: index_eqn over every tile
             if bands_in:
-                e0 = e1 = None
-                if timed:
-                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(
-                        enable_timing=True)
-                    e0.record()
-                values.append(eng.index_tile(index_fn, sc.bands[:, :, p0:p1],
-                                             out=index_buf[:, p0:p1]))
-                if timed:
-                    e1.record()
-                    idx_events.append((e0, e1))
+                with torch.cuda.stream(load_stream if load_stream is not None else main):
+                    e0 = e1 = None
+                    if timed:
+                        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(
+                            enable_timing=True)
+                        e0.record()
+                    values.append(eng.index_tile(index_fn, sc.bands[:, :, p0:p1],
+                                                 out=index_buf[:, p0:p1]))
+                    if timed:
+                        e1.record()
+                        idx_events.append((e0, e1))
+                    ev = None
+                    if load_stream is not None:
+                        ev = torch.cuda.Event()
+                        ev.record()
+                    ready.append(ev)
             else:
                 values.append(sc.values[:, p0:p1])
+                ready.append(None)
         for g0 in range(0, len(tiles), group):
             ts = range(g0, min(len(tiles), g0 + group))
             # analyze + label (tile t's resolve stage beside tile t+1's analyze stage)
@@ -221,7 +239,8 @@ def main():
                 [(values[t], sc.valid[:, tiles[t][0]:tiles[t][1]] if sc.valid is not None
                   else None) for t in ts], fields,
                 outs=[{f: x[..., :tiles[t][1] - tiles[t][0]] for f, x in slabs[t].items()}
-                      for t in ts])
+                      for t in ts],
+                ready=[ready[t] for t in ts] if load_stream is not None else None)
             if gather:  # these tiles' label rasters to the writer rank, on
                 # RCCL's stream: they travel while the next group computes
                 for t in ts:
@@ -313,6 +332,9 @@ def main():
         'load_stage': None if index_ms is None else {
             'kernel': 'lt_index_kernel (hiprtc, index_eqn "B1 - B2", int16 bands -> int16)',
             'ms_per_launch': round(index_ms, 3),
+            # on its own stream the index kernels share the CUs with analyze kernels, so a
+            # launch lasts longer than alone (--serial-load: 0.13 ms, 5.5 TB/s on c2)
+            'overlapped_with_analyze': load_stream is not None,
             'hbm_gbs_algorithmic': round(meta.n_obs * 6 * px_per_launch / (index_ms * 1e-3) / 1e9,
                                          1)},
         'resolve_stage': {'ms_per_launch': round(resolve_ms, 3),

@@ -201,6 +201,14 @@ int lt_analyze_tile(lt_ctx* ctx, const lt_scene* scene, const lt_params* params,
 int lt_analyze_tiles(lt_ctx* ctx, const lt_scene* scene, const lt_params* params, int n_tiles,
                      const lt_tile_in* ins, const lt_tile_out* outs, void* stream);
 
+/* lt_analyze_tiles where tile t's analyze kernel first waits on ready[t] (a recorded hipEvent_t,
+ * or NULL = no wait; `ready` itself may be NULL). The load stage (parse_mapper's rast_algebra,
+ * utils.py:447-484) of later tiles can then run on another stream beside this call's analyze
+ * kernels instead of all of it ahead of the call. */
+int lt_analyze_tiles_after(lt_ctx* ctx, const lt_scene* scene, const lt_params* params,
+                           int n_tiles, const lt_tile_in* ins, const lt_tile_out* outs,
+                           void* const* ready, void* stream);
+
 /* change_labeling alone (utils.py:795-820) on trendlines already in device memory. Writes the
  * rule planes of `out` and out->status (only LT_ST_PRE_THRESHOLD_ATTR can be set). */
 int lt_label_tile(lt_ctx* ctx, const lt_label_in* in, const lt_params* params,

@@ -105,7 +105,7 @@ PIX_FIELDS = [('status', 'int32'), ('n_years', 'int32')]
 
 # symbols include/lt_abi.h declares (checked by tests/test_abi.py)
 EXPORTS = ['lt_abi_version', 'lt_ctx_create', 'lt_ctx_destroy', 'lt_last_error',
-           'lt_analyze_tile', 'lt_analyze_tiles', 'lt_label_tile', 'lt_ctx_set_timing', 'lt_ctx_stage_ms',
+           'lt_analyze_tile', 'lt_analyze_tiles', 'lt_analyze_tiles_after', 'lt_label_tile', 'lt_ctx_set_timing', 'lt_ctx_stage_ms',
            'lt_ctx_last_deferred', 'lt_index_codegen', 'lt_index_compile', 'lt_index_apply']
 
 _LIB = None
@@ -133,6 +133,9 @@ def load_lib(path=None):
     lib.lt_analyze_tiles.argtypes = [vp, ctypes.POINTER(LtScene), ctypes.POINTER(LtParams),
                                      ctypes.c_int, ctypes.POINTER(LtTileIn),
                                      ctypes.POINTER(LtTileOut), vp]
+    lib.lt_analyze_tiles_after.argtypes = [vp, ctypes.POINTER(LtScene), ctypes.POINTER(LtParams),
+                                           ctypes.c_int, ctypes.POINTER(LtTileIn),
+                                           ctypes.POINTER(LtTileOut), ctypes.POINTER(vp), vp]
     lib.lt_label_tile.argtypes = [vp, ctypes.POINTER(LtLabelIn), ctypes.POINTER(LtParams),
                                   ctypes.POINTER(LtTileOut), vp]
     lib.lt_ctx_set_timing.argtypes = [vp, ctypes.c_int]

@@ -385,6 +385,12 @@ static int launch_tile(lt_ctx* c, const lt_params* prm, const lt_tile_in* in,
 
 int lt_analyze_tiles(lt_ctx* c, const lt_scene* sc, const lt_params* prm, int n_tiles,
                      const lt_tile_in* ins, const lt_tile_out* outs, void* stream_) {
+  return lt_analyze_tiles_after(c, sc, prm, n_tiles, ins, outs, nullptr, stream_);
+}
+
+int lt_analyze_tiles_after(lt_ctx* c, const lt_scene* sc, const lt_params* prm, int n_tiles,
+                           const lt_tile_in* ins, const lt_tile_out* outs, void* const* ready,
+                           void* stream_) {
   if (!c) return LT_ERR_ARG;
   if (!sc || !prm || n_tiles < 0 || (n_tiles > 0 && (!ins || !outs)))
     return fail(c, LT_ERR_ARG, "null argument%s");
@@ -469,6 +475,7 @@ int lt_analyze_tiles(lt_ctx* c, const lt_scene* sc, const lt_params* prm, int n_
     if (ins[t].n_pix == 0) continue;
     const int set = t & 1;
     if (c->set_used[set]) HIP_OR_FAIL(c, hipStreamWaitEvent(stream, c->ev_resolved[set], 0));
+    if (ready && ready[t]) HIP_OR_FAIL(c, hipStreamWaitEvent(stream, (hipEvent_t)ready[t], 0));
     const int rc = launch_tile(c, prm, &ins[t], &outs[t], Y, stream, c->side, set);
     if (rc != LT_OK) return rc;
     c->set_used[set] = true;

@@ -85,10 +85,13 @@ class Engine:
         self._check(rc, 'lt_analyze_tile')
         return out
 
-    def analyze_tiles(self, scene, params, tiles, fields=ALL_FIELDS, outs=None, stream=None):
+    def analyze_tiles(self, scene, params, tiles, fields=ALL_FIELDS, outs=None, stream=None,
+                      ready=None):
         """analyze_tile over a list of (values, valid) tiles of one scene in one call
-        (lt_analyze_tiles: tile t's resolve stage overlaps tile t+1's analyze stage). Returns the
-        list of output dicts; asynchronous on `stream`."""
+        (lt_analyze_tiles: tile t's resolve stage overlaps tile t+1's analyze stage). ready: None
+        or one recorded torch.cuda.Event (or None) per tile, which that tile's analyze kernel
+        waits on (lt_analyze_tiles_after: the load stage of later tiles may still be running on
+        another stream). Returns the list of output dicts; asynchronous on `stream`."""
         n = len(tiles)
         tins = (_abi.LtTileIn * max(n, 1))()
         touts = (_abi.LtTileOut * max(n, 1))()
@@ -101,8 +104,17 @@ class Engine:
             res.append(o)
         sc = scene.to_c()
         st = stream if stream is not None else torch.cuda.current_stream(self.device)
-        rc = self.lib.lt_analyze_tiles(self.ctx, ctypes.byref(sc), ctypes.byref(params), n, tins,
-                                       touts, ctypes.c_void_p(st.cuda_stream))
+        if ready is None:
+            rc = self.lib.lt_analyze_tiles(self.ctx, ctypes.byref(sc), ctypes.byref(params), n,
+                                           tins, touts, ctypes.c_void_p(st.cuda_stream))
+        else:
+            if len(ready) != n:
+                raise LtError('ready needs one event (or None) per tile')
+            evs = (ctypes.c_void_p * max(n, 1))(
+                *[e.cuda_event if e is not None else None for e in ready])
+            rc = self.lib.lt_analyze_tiles_after(self.ctx, ctypes.byref(sc), ctypes.byref(params),
+                                                 n, tins, touts, evs,
+                                                 ctypes.c_void_p(st.cuda_stream))
         self._check(rc, 'lt_analyze_tiles')
         return res
 

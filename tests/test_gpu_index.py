@@ -127,3 +127,50 @@ def test_analysis_reducer_batch_from_bands(engine):
     b = analysis_reducer_batch(sc.dates, sc.values.to(dev), None, settings)
     for f in ('status', 'matched', 'class_val', 'onset_year', 'duration', 'magnitude'):
         assert torch.equal(a[f], b[f]), f
+
+def test_load_stage_on_own_stream_with_ready_events(engine):
+    """Tile t's index raster written on a load stream, its analyze kernel waiting on tile t's
+    event alone (lt_analyze_tiles_after): bit-exact against the oracle on float(index), and
+    equal to the serial bands -> index -> lt_analyze_tiles order."""
+    from land_trendr_amd.synth import make_scene
+    from oracle import oracle
+    sc = make_scene(24000, seed=33, n_years=30, k_min=1, k_max=2, mask_prob=0.1,
+                    with_bands=True)
+    meta = build_scene(sc.dates, parse_date('2014-07-01'))
+    params, _ = compile_params(10.0, [{'name': 'gd', 'val': 1, 'change_type': 'GD'}])
+    fn = engine.compile_index(index_eqn.IndexProgram('B1 - B2', band_dtype=np.int16))
+    dev = engine.device
+    bands, valid = sc.bands.to(dev), sc.valid.to(dev)
+    K, _, P = bands.shape
+    cuts = [0, 5000, 11000, 11001, 24000]  # uneven tiles, one of a single pixel
+    spans = list(zip(cuts[:-1], cuts[1:]))
+    main = torch.cuda.current_stream(dev)
+    load = torch.cuda.Stream(dev)
+    load.wait_stream(main)
+    index = torch.empty((K, P), dtype=torch.int16, device=dev)
+    ready = []
+    with torch.cuda.stream(load):
+        for a, b in spans:
+            engine.index_tile(fn, bands[:, :, a:b], out=index[:, a:b])
+            ev = torch.cuda.Event()
+            ev.record()
+            ready.append(ev)
+    tiles = [(index[:, a:b], valid[:, a:b]) for a, b in spans]
+    over = engine.analyze_tiles(meta, params, tiles, ready=ready)
+    torch.cuda.synchronize()
+    serial_index = engine.index_tile(fn, bands)
+    serial = engine.analyze_tiles(meta, params, [(serial_index[:, a:b], valid[:, a:b])
+                                                 for a, b in spans])
+    torch.cuda.synchronize()
+    assert torch.equal(index, serial_index)
+    vals = serial_index.cpu().numpy().astype(np.float64)
+    want = oracle.analyze_tile(meta, params, vals, sc.valid.numpy(),
+                               n_threads=os.cpu_count() or 1)
+    for (a, b), o, s in zip(spans, over, serial):
+        for f in o:
+            x, y = o[f].cpu().numpy(), s[f].cpu().numpy()
+            assert x.tobytes() == y.tobytes(), (a, b, f)
+            if f in ('class_val', 'onset_year', 'duration', 'magnitude', 'initial_val'):
+                continue  # unmatched slots hold no defined value
+            same = _bits_equal(want[f][..., a:b], x)
+            assert same.all(), (a, b, f, int((~same).sum()))
