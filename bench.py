@@ -132,7 +132,9 @@ def main():
     ap.add_argument('--warmup', type=int, default=1)
     ap.add_argument('--config', default='c2', choices=sorted(CONFIGS))
     ap.add_argument('--pixels', type=int, default=0, help='pixels per GPU (default: config)')
-    ap.add_argument('--tile', type=int, default=1 << 22, help='pixels per launch')
+    ap.add_argument('--tile', type=int, default=0,
+                    help='pixels per launch (0: 1<<24 alone, 1<<22 when label rasters are '
+                         'gathered, so each group of 4 tiles is gathered while the next computes)')
     ap.add_argument('--no-gather', action='store_true',
                     help='N>1: skip the RCCL gather of label rasters to rank 0')
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
@@ -185,11 +187,15 @@ def main():
     if cfg['trendline']:
         fields += ['winner', 'val_raw', 'val_fit', 'fit_m', 'fit_b', 'right_m', 'right_b',
                    'spike', 'vertex']
+    gather = dist is not None and not args.no_gather
+    if args.tile <= 0:
+        # c2 sweep on one MI355X (profiles/r01_c2_tile_sweep.txt): 2 Mpx 1459, 4 Mpx 1569,
+        # 8 Mpx 1627, 16 Mpx 1647, 25 Mpx 1650, one 49 Mpx tile 1629 Mpx/s — fewer launch tails
+        args.tile = 1 << 22 if gather else 1 << 24
     tiles = [(p0, min(P, p0 + args.tile)) for p0 in range(0, P, args.tile)]
     # tile-major output planes: tile t's [R|Y, tile] slab of every field is contiguous, so it can
     # be handed to RCCL as soon as its kernels are queued
     slabs = [eng.alloc_outputs(meta.n_years, params.n_rules, args.tile, fields) for _ in tiles]
-    gather = dist is not None and not args.no_gather
     recv = None
     if gather and rank == 0:  # the writer's label rasters for the whole job, allocated once
         recv = {f: [[torch.empty_like(sl[f]) for sl in slabs] for _ in range(world)]

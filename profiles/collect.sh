@@ -11,6 +11,6 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/k
   python3 $R/bench.py --steps 3 --warmup 1 > $OUT/bench_default.json 2> $OUT/bench_default.err
 echo "kernel trace ok"
 cd $R
-timeout -k 10 600 bash profiles/pmc_passes.sh ${1}/pmc --pixels 4194304 --steps 1 --warmup 0
-python3 profiles/summarize_pmc.py $OUT/pmc $OUT/pmc_c2.json 4194304 > /dev/null
+timeout -k 10 600 bash profiles/pmc_passes.sh ${1}/pmc --pixels 16777216 --steps 1 --warmup 0
+python3 profiles/summarize_pmc.py $OUT/pmc $OUT/pmc_c2.json 16777216 > /dev/null
 echo "pmc ok"
