@@ -54,11 +54,14 @@ __device__ inline void defer_append(bool deferred, int64_t p, int lane, int64_t*
 
 // Stage 1 (wave-lockstep body, lt_fast.h): one wave per workgroup, the pixel series in LDS.
 // Occupancy target: 4 waves per SIMD (<= 128 VGPRs) where the body fits without spilling.
+#ifndef LT_FAST_WAVES_C2  // waves per SIMD the single-rule MAXY <= 32 instance is built for
+#define LT_FAST_WAVES_C2 4
+#endif
 #ifndef LT_FAST_WAVES_BIG
 #define LT_FAST_WAVES_BIG 4
 #endif
 template <int MAXY, int RMAX>
-__global__ __launch_bounds__(64, (MAXY <= 32 && RMAX == 1) ? 4 : LT_FAST_WAVES_BIG) void analyze_fast_kernel(const lt::DevScene* __restrict__ S,
+__global__ __launch_bounds__(64, (MAXY <= 32 && RMAX == 1) ? LT_FAST_WAVES_C2 : LT_FAST_WAVES_BIG) void analyze_fast_kernel(const lt::DevScene* __restrict__ S,
                                                           const lt_params P, const lt_tile_in in,
                                                           const lt_tile_out out,
                                                           const lt::lsq_xf* __restrict__ xtab,
