@@ -133,12 +133,13 @@ def main():
     ap.add_argument('--config', default='c2', choices=sorted(CONFIGS))
     ap.add_argument('--pixels', type=int, default=0, help='pixels per GPU (default: config)')
     ap.add_argument('--tile', type=int, default=0,
-                    help='pixels per launch (0: 1<<24 alone, 1<<22 when label rasters are '
-                         'gathered, so each group of 4 tiles is gathered while the next computes)')
+                    help='pixels per launch (0: 1<<24)')
     ap.add_argument('--no-gather', action='store_true',
                     help='N>1: skip the RCCL gather of label rasters to rank 0')
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--group', type=int, default=0,
+                    help='tiles per lt_analyze_tiles call (0: all, or 1 when gathering)')
     ap.add_argument('--serial-load', action='store_true',
                     help='run every tile\'s index_eqn kernel ahead of the analyze kernels on '
                          'one stream (default: load stage on its own stream, per-tile events)')
@@ -191,7 +192,7 @@ def main():
     if args.tile <= 0:
         # c2 sweep on one MI355X (profiles/r01_c2_tile_sweep.txt): 2 Mpx 1459, 4 Mpx 1569,
         # 8 Mpx 1627, 16 Mpx 1647, 25 Mpx 1650, one 49 Mpx tile 1629 Mpx/s — fewer launch tails
-        args.tile = 1 << 22 if gather else 1 << 24
+        args.tile = 1 << 24
     tiles = [(p0, min(P, p0 + args.tile)) for p0 in range(0, P, args.tile)]
     # tile-major output planes: tile t's [R|Y, tile] slab of every field is contiguous, so it can
     # be handed to RCCL as soon as its kernels are queued
@@ -204,7 +205,10 @@ def main():
 
     # tiles per lt_analyze_tiles call: all of them, or groups whose label rasters go to RCCL
     # while the next group computes
-    group = len(tiles) if not gather else 4
+    # (gathering: one tile per call, so tile t's label rasters travel while tile t+1 computes;
+    # N=1 layout proxies on one MI355X: 16.8 Mpx x 1 per call 1629, 8.4 Mpx x 2 1613, 4.19 Mpx
+    # x 4 1554 Mpx/s, profiles/r01_c2_tile_sweep.txt)
+    group = args.group if args.group > 0 else (len(tiles) if not gather else 1)
 
     # the load stage runs on its own stream: tile t's analyze kernel waits only for tile t's
     # index raster, so later tiles' index kernels (HBM-bound) run beside earlier tiles' analyze
