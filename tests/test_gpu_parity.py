@@ -106,9 +106,9 @@ def test_tie_heavy_small_integers_tiny_line_cost_vs_oracle(engine):
 
 @pytest.mark.parametrize('cfg', ['c2', 'c3', 'c5'])
 def test_full_size_scene_sampled_vs_oracle(engine, cfg):
-    """BASELINE.json sizes: a 7000x7000-pixel scene per config analysed on the GPU in 4 Mpx
-    tiles (as bench.py does); 20,000 random pixels re-analysed by the oracle must agree bit for
-    bit, every pixel's status must be 0 (no unemulated path), and the label rasters must be
+    """BASELINE.json sizes: a 7000x7000-pixel scene per config analysed on the GPU in 16.8 Mpx
+    tiles (bench.py's default); 200,000 random pixels re-analysed by the oracle must agree bit
+    for bit, every pixel's status must be 0 (no unemulated path), and the label rasters must be
     internally consistent (matched <=> class_val/onset/duration/magnitude set)."""
     import bench
     from land_trendr_amd.synth import make_scene
@@ -122,7 +122,7 @@ def test_full_size_scene_sampled_vs_oracle(engine, cfg):
     fields = ('status', 'matched', 'class_val', 'onset_year', 'duration', 'magnitude',
               'val_fit', 'vertex')
     out = engine.alloc_outputs(meta.n_years, params.n_rules, P, fields)
-    tile = 1 << 22
+    tile = 1 << 24
     spans = [(p0, min(P, p0 + tile)) for p0 in range(0, P, tile)]
     # one batched call, as bench.py makes it (tile t's resolve beside tile t+1's analyze)
     engine.analyze_tiles(meta, params,
@@ -134,7 +134,7 @@ def test_full_size_scene_sampled_vs_oracle(engine, cfg):
     m = out['matched'].bool()
     assert bool(((out['class_val'] != -99) == m).all())
     assert bool(((out['duration'] > 0) | ~m).all())
-    idx = torch.from_numpy(np.random.default_rng(7).choice(P, 20000, replace=False)).to(
+    idx = torch.from_numpy(np.random.default_rng(7).choice(P, 200000, replace=False)).to(
         engine.device)
     vals = sc.values[:, idx].cpu().numpy()
     valid = sc.valid[:, idx].cpu().numpy() if sc.valid is not None else None
