@@ -8,6 +8,7 @@ fitted values and the vertex flags bit for bit. Prints one progress line per chu
 JSON summary.
 
 Usage (GPU box): python tests/full_scene_check.py --config c2 --out gpurun_out/full_c2.json
+(--first/--last: re-analyse one pixel range of the whole scene, to split a long check in calls)
 """
 import argparse
 import json
@@ -38,6 +39,8 @@ def main():
     ap.add_argument('--config', default='c2', choices=sorted(bench.CONFIGS))
     ap.add_argument('--pixels', type=int, default=0)
     ap.add_argument('--chunk', type=int, default=1 << 21)
+    ap.add_argument('--first', type=int, default=0, help='first pixel the oracle re-analyses')
+    ap.add_argument('--last', type=int, default=0, help='end of that range (0: the scene end)')
     ap.add_argument('--out', default='')
     args = ap.parse_args()
     c = bench.CONFIGS[args.config]
@@ -74,8 +77,9 @@ def main():
     assert torch.equal(index.to(torch.float64), sc.values), 'index raster != synthetic index'
     threads = min(len(os.sched_getaffinity(0)), 64)
     diff = {f: 0 for f in FIELDS}
-    for a in range(0, P, args.chunk):
-        b = min(P, a + args.chunk)
+    end = args.last or P
+    for a in range(args.first, end, args.chunk):
+        b = min(end, a + args.chunk)
         vals = sc.values[:, a:b].cpu().numpy()
         valid = sc.valid[:, a:b].cpu().numpy() if sc.valid is not None else None
         want = oracle.analyze_tile(meta, params, vals, valid, n_threads=threads)
@@ -85,8 +89,9 @@ def main():
                     if x.dtype.kind == 'f' else x == y)
             diff[f] += int((~same).sum())
         print('oracle %d/%d px, differing values so far %d, %.0f s' % (
-            b, P, sum(diff.values()), time.time() - t0), flush=True)
-    res = {'config': args.config, 'pixels': P, 'tile_pixels': tile, 'seed': 1000,
+            b, end, sum(diff.values()), time.time() - t0), flush=True)
+    res = {'config': args.config, 'pixels': P, 'checked': [args.first, end],
+           'tile_pixels': tile, 'seed': 1000,
            'input': 'int16 bands + index_eqn "B1 - B2" (bench.py rank 0 scene)',
            'fields': list(FIELDS), 'differing_values': diff,
            'bit_exact': sum(diff.values()) == 0, 'oracle_threads': threads,
