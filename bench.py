@@ -1,16 +1,18 @@
-"""Benchmark: full LandTrendr analyze + label of a Landsat-scene-sized stack per GPU.
+"""Benchmark: full LandTrendr analyze + label of Landsat-scene-sized stacks on 1..N GPUs.
 
 Metric (BASELINE.json): Mpixels/s of full analyze (30-yr series), whole job over all GPUs, with
-the FP64-VALU roofline fraction of the dominant kernel. Default workload = configs[1] (c2):
-7000 x 7000 px x 30 years, 1 obs/yr, one GD rule, line_cost 10, on one MI355X. Inputs are
-synthetic, generated directly in HBM before the timed region.
+the roofline fraction of the dominant kernel. Default workload = configs[1] (c2): one
+7000 x 7000 px x 30 year scene per GPU, 1 obs/yr, one GD rule, line_cost 10 (weak scaling).
+--config c4 = configs[3]: ONE 4-scene mosaic (4 x 49 Mpx x 30 yr) whose pixel tiles are dealt
+round-robin to the ranks (strong scaling). Inputs are synthetic, int16 bands
+generated in HBM before the timed region.
 
-A step = one pass of the hot path over the rank's whole scene, as a queue of pixel tiles
-(lt_analyze_tile launches on the current stream). Multi-GPU (torchrun, one process per GPU):
-each rank analyses its own scene (weak scaling, no data-path collective) and gathers each tile's
-label rasters to rank 0 over RCCL inside the step, asynchronously, so the transfer of tile t runs
-while tile t+1 computes (the reference's output_reducer input; --no-gather
-drops it).
+A step = one pass of the hot path over the job (land_trendr_amd/runner.py, the code path the job
+runner uses too): per tile, the index_eqn load kernel (B1 - B2) on the load stream, analyze +
+label, then the tile's label rasters sent point-to-point to rank 0 over RCCL (N > 1), travelling
+while the next tile computes. After the timed steps: the load kernel timed alone (its HBM
+roofline) and, unless --e2e-steps 0, end-to-end steps that add H2D of the pinned int16 bands and
+D2H of the label rasters (and, for c5, of every per-year trendline plane) to the same pipeline.
 """
 import argparse
 import json
@@ -23,14 +25,20 @@ import torch
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from land_trendr_amd.distributed import LABEL_GATHER_FIELDS  # noqa: E402
+from land_trendr_amd.distributed import Mosaic, TrendlineStream  # noqa: E402
 from land_trendr_amd.engine import get_engine  # noqa: E402
+from land_trendr_amd.index_eqn import IndexProgram  # noqa: E402
+from land_trendr_amd.runner import MosaicRunner  # noqa: E402
 from land_trendr_amd.scene import build_scene, parse_date  # noqa: E402
 from land_trendr_amd.settings import compile_params  # noqa: E402
-from land_trendr_amd.synth import make_scene  # noqa: E402
+from land_trendr_amd.synth import make_scene, mosaic_inputs  # noqa: E402
 
-FP64_PEAK_TFLOPS = 78.6     # MI355X FP64 vector peak (spec)
-HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md chip-level parameters
+# MI355X peaks (MI355X_MICROARCH.md)
+FP64_PEAK_TFLOPS = 78.6          # 256 CUs x 4 SIMDs x 16 lanes x 2 (FMA) x 2.4 GHz
+HBM_PEAK_GBS = 8000.0
+SIMDS, CLOCK_GHZ, CYC_PER_VALU = 1024, 2.4, 4
+VALU_PEAK_G = SIMDS * CLOCK_GHZ / CYC_PER_VALU  # 614.4 G wave64 VALU instructions/s
+TARGET = '2014-07-01'
 
 GD = [{'name': 'gd', 'val': 1, 'change_type': 'GD'}]
 C3_RULES = [{'name': 'fd', 'val': 2, 'change_type': 'FD', 'onset_year': ['>=', 1995],
@@ -40,14 +48,20 @@ C3_RULES = [{'name': 'fd', 'val': 2, 'change_type': 'FD', 'onset_year': ['>=', 1
 CONFIGS = {
     'c2': dict(desc='c2: 7000x7000 px x 30 yr, 1 obs/yr, GD rule, line_cost 10', pixels=49_000_000,
                years=30, k=(1, 1), mask=0.0, line_cost=10.0, rules=GD, mode='reference',
-               trendline=False),
+               trendline=False, seed=1000),
     'c3': dict(desc='c3: 7000x7000 px x 30 yr, 1-4 obs/yr + cloud masks, FD/GD/LD rules',
                pixels=49_000_000, years=30, k=(1, 4), mask=0.2, line_cost=10.0, rules=C3_RULES,
-               mode='documented', trendline=False),
+               mode='documented', trendline=False, seed=1000),
+    'c4': dict(desc='c4: 4-scene mosaic (4 x 7000x7000 px = 196 Mpx) x 30 yr, GD rule, '
+                    'line_cost 10, tiles round-robin over the GPUs', pixels=49_000_000, scenes=4,
+               years=30, k=(1, 1), mask=0.0, line_cost=10.0, rules=GD, mode='reference',
+               trendline=False, seed=4000),
     'c5': dict(desc='c5: 40-yr series, line_cost 1, full per-year trendline output',
                pixels=49_000_000, years=40, k=(1, 1), mask=0.0, line_cost=1.0, rules=GD,
-               mode='reference', trendline=True),
+               mode='reference', trendline=True, seed=1000),
 }
+TRENDLINE_FIELDS = ['winner', 'val_raw', 'val_fit', 'fit_m', 'fit_b', 'right_m', 'right_b',
+                    'spike', 'vertex']
 
 
 def f_ref(n):
@@ -56,61 +70,64 @@ def f_ref(n):
     return 20 * s3 + n * (n + 1) + 24 * n
 
 
-def bytes_per_pixel(cfg, n_obs, n_years, value_bytes=8):
-    inp = n_obs * value_bytes + (n_obs if cfg['mask'] > 0 else 0)  # index values + mask
+def bytes_per_pixel(cfg, n_obs, n_years):
+    """Algorithmic HBM bytes per pixel of the analyze kernel: the int16 index raster (+ mask),
+    the label planes, the per-year planes when the config asks for them, status."""
+    inp = n_obs * 2 + (n_obs if cfg['mask'] > 0 else 0)
     lab = len(cfg['rules']) * (1 + 4 + 4 + 4 + 8)                 # matched/class/onset/dur/mag
     tl = n_years * (6 * 8 + 2 + 2) if cfg['trendline'] else 0     # 6 f64 + spike/vertex + winner
-    return inp + lab + tl + 4                                     # + status
+    return inp + lab + tl + 4
 
 
-PMC_SUMMARY = os.path.join(ROOT, 'profiles', 'r01_pmc_c2.json')
-
-
-def pmc_traffic(kernel, px_per_launch, input_mode):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc summary of this build
-    (FETCH_SIZE/WRITE_SIZE passes, gfx950-corrected: profiles/summarize_pmc.py), scaled to this
-    launch's pixel count; None when absent."""
+def pmc_summary(config):
+    """The committed rocprofv3 --pmc summary of this build for `config` (profiles/
+    summarize_pmc.py: per-launch counters of one 16.8 Mpx launch; c4 runs c2's kernel instance)."""
+    name = {'c4': 'c2'}.get(config, config)
+    path = os.path.join(ROOT, 'profiles', 'r02_pmc_%s.json' % name)
     try:
-        with open(PMC_SUMMARY) as f:
+        with open(path) as f:
             d = json.load(f)
-        if d.get('_input', 'index') != input_mode:
-            return None
-        return d[kernel]['hbm_bytes'] / d['_pixels_per_launch'] * px_per_launch
-    except (OSError, KeyError, ValueError, TypeError, ZeroDivisionError):
+        d['_path'] = os.path.relpath(path, ROOT)
+        return d
+    except (OSError, ValueError):
         return None
 
 
-def pmc_fp64_issued(kernel, px_per_launch, input_mode):
-    """FP64 flops the hardware issued per launch of `kernel` (PMC SQ_INSTS_VALU_{ADD,MUL,FMA}_F64
-    x 64 lanes, FMA = 2) from the committed summary, scaled to this launch's pixel count."""
+def per_px(pmc, kernel, counter):
     try:
-        with open(PMC_SUMMARY) as f:
-            d = json.load(f)
-        if d.get('_input', 'index') != input_mode:
-            return None
-        k = d[kernel]
-        wave_flops = (k['SQ_INSTS_VALU_ADD_F64'] + k['SQ_INSTS_VALU_MUL_F64'] +
-                      2 * k['SQ_INSTS_VALU_FMA_F64'])
-        return 64 * wave_flops / d['_pixels_per_launch'] * px_per_launch
-    except (OSError, KeyError, ValueError, TypeError, ZeroDivisionError):
+        return pmc[kernel][counter] / pmc['_pixels_per_launch']
+    except (KeyError, TypeError, ZeroDivisionError):
         return None
+
+
+def host_cores():
+    """Threads this process may run on, and the CPUs its cgroup quota grants (the GPU box shows
+    the whole machine's CPUs but gives each job a share)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    quota = None
+    try:
+        q, per = open('/sys/fs/cgroup/cpu.max').read().split()[:2]
+        if q != 'max':
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    return n, quota
 
 
 def cpu_baseline(cfg, seconds):
-    """The oracle (C restatement, pthreads over all host cores) on a bounded sample."""
+    """The oracle (C restatement, pthreads over every host core this process may use) on a
+    bounded sample of the same configuration."""
     from oracle import oracle
-    threads = os.cpu_count() or 1
-    try:
-        threads = len(os.sched_getaffinity(0))
-    except AttributeError:
-        pass
-    threads = min(threads, 64)
+    threads, quota = host_cores()
     sample = max(64, 16 * threads)
     rate = None
     while True:
         sc = make_scene(sample, n_years=cfg['years'], k_min=cfg['k'][0], k_max=cfg['k'][1],
                         mask_prob=cfg['mask'], seed=77, device='cpu')
-        meta = build_scene(sc.dates, parse_date('2014-07-01'))
+        meta = build_scene(sc.dates, parse_date(TARGET))
         params, _ = compile_params(cfg['line_cost'], cfg['rules'], cfg['mode'])
         vals = sc.values.numpy()
         valid = sc.valid.numpy() if sc.valid is not None else None
@@ -118,11 +135,78 @@ def cpu_baseline(cfg, seconds):
         oracle.analyze_tile(meta, params, vals, valid, n_threads=threads)
         dt = time.perf_counter() - t0
         rate = sample / dt
-        if dt >= 0.5 * seconds or sample >= 2_000_000:
+        if dt >= 0.5 * seconds or sample >= 4_000_000:
             break
-        sample = int(min(2_000_000, max(sample * 2, rate * seconds)))
-    return {'value': rate / 1e6, 'unit': 'Mpixels/s', 'cores': threads, 'kind': 'port',
-            'sample': '%d synthetic px of the same config, oracle/lt_oracle.c, %.1f s' % (sample, dt)}
+        sample = int(min(4_000_000, max(sample * 2, rate * seconds)))
+    cores = threads if quota is None else min(threads, quota)
+    return {'value': rate / 1e6, 'unit': 'Mpixels/s', 'cores': round(cores, 2), 'kind': 'port',
+            'threads': threads, 'cgroup_cpu_quota': quota,
+            'sample': '%d synthetic px of the same config, oracle/lt_oracle.c, %d threads, %.1f s'
+                      % (sample, threads, dt)}
+
+
+class _PinnedBands:
+    """stage_in for MosaicRunner.step: tile k's int16 bands H2D from pinned host memory into
+    device slab k % 2 on a copy stream, once the load kernel of tile k - 2 has read that slab."""
+
+    def __init__(self, items, dev):
+        self.host = [it.bands.cpu().pin_memory() for it in items]
+        big = max(self.host, key=lambda b: b.numel())
+        self.slab = [torch.empty(big.shape, dtype=torch.int16, device=dev) for _ in range(2)]
+        self.free = [None, None]
+        self.stream = torch.cuda.Stream(dev)
+        self.bytes = 0
+
+    def fetch(self, k):
+        s = k % 2
+        h = self.host[k]
+        with torch.cuda.stream(self.stream):
+            if self.free[s] is not None:
+                self.stream.wait_event(self.free[s])
+            dst = self.slab[s][:, :, :h.shape[2]]
+            dst.copy_(h, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+        self.bytes += h.numel() * h.element_size()
+        return dst, ev
+
+    def consumed(self, k, ev):
+        self.free[k % 2] = ev
+
+
+def end_to_end(runner, cfg, steps):
+    """Steps of the same pipeline with the data movement a job has: each tile's int16 bands H2D
+    from pinned host memory before its load kernel (_PinnedBands), the writer's label rasters
+    D2H after the exchange, and for trendline configs every per-year plane of every tile D2H
+    through TrendlineStream (tile k-1's planes queued behind tile k's kernels).
+    Returns (seconds, H2D bytes, D2H bytes)."""
+    dev = runner.eng.device
+    stage = _PinnedBands(runner.items, dev)
+    d2h = TrendlineStream(runner.m.tile * 8, dev, depth=8) if cfg['trendline'] else None
+    ex = runner.exchange
+    lab_host = ({f: torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+                 for f, t in ex.full.items()} if ex.is_writer else {})
+    items = runner.items
+    bytes_d2h = 0
+
+    def after(k):
+        if d2h is not None and k > 0:
+            d2h.push({f: runner.outs[k - 1][f] for f in TRENDLINE_FIELDS}, items[k - 1].tile.n)
+
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        runner.step(after_tile=after, stage_in=stage)
+        if d2h is not None:
+            d2h.push({f: runner.outs[-1][f] for f in TRENDLINE_FIELDS}, items[-1].tile.n)
+        for f, t in lab_host.items():  # the writer's label rasters, for its GeoTIFF writer
+            t.copy_(ex.full[f], non_blocking=True)
+            bytes_d2h += t.numel() * t.element_size()
+        torch.cuda.synchronize()
+        if d2h is not None:
+            d2h.drain()
+    dt = time.perf_counter() - t0
+    return dt, stage.bytes, bytes_d2h + (d2h.bytes if d2h is not None else 0)
 
 
 def main():
@@ -131,21 +215,19 @@ def main():
     ap.add_argument('--steps', type=int, default=3)
     ap.add_argument('--warmup', type=int, default=1)
     ap.add_argument('--config', default='c2', choices=sorted(CONFIGS))
-    ap.add_argument('--pixels', type=int, default=0, help='pixels per GPU (default: config)')
+    ap.add_argument('--pixels', type=int, default=0, help='pixels per scene (default: config)')
     ap.add_argument('--tile', type=int, default=0,
-                    help='pixels per launch (0: 1<<24)')
+                    help='pixels per tile (0: 1<<24, or scene/8 for the c4 mosaic)')
     ap.add_argument('--no-gather', action='store_true',
-                    help='N>1: skip the RCCL gather of label rasters to rank 0')
+                    help='N>1: skip the exchange of label rasters to rank 0')
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--e2e-steps', type=int, default=1,
+                    help='end-to-end steps (H2D bands, D2H outputs) after the timed ones; 0: none')
     ap.add_argument('--group', type=int, default=0,
-                    help='tiles per lt_analyze_tiles call (0: all, or 1 when gathering)')
+                    help='tiles per lt_analyze_tiles call (0: all of a scene, or 1 when gathering)')
     ap.add_argument('--serial-load', action='store_true',
-                    help='run every tile\'s index_eqn kernel ahead of the analyze kernels on '
-                         'one stream (default: load stage on its own stream, per-tile events)')
-    ap.add_argument('--input', default='bands', choices=['bands', 'index'],
-                    help='bands: int16 B1, B2 planes + index_eqn "B1 - B2" on the GPU (the '
-                         'reference pipeline, SURVEY.md 8(d)); index: float64 index values')
+                    help='run the index_eqn kernels on the analyze stream (no load stream)')
     args = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -166,104 +248,29 @@ def main():
     cfg = CONFIGS[args.config]
     P = args.pixels or cfg['pixels']
     dev = torch.device('cuda', local)
-
-    bands_in = args.input == 'bands'
-    sc = make_scene(P, n_years=cfg['years'], k_min=cfg['k'][0], k_max=cfg['k'][1],
-                    mask_prob=cfg['mask'], seed=1000 + rank, device=dev, with_bands=bands_in)
-    index_fn = index_buf = None
-    if bands_in:  # the load stage: settings.json index_eqn on int16 bands, compiled with hiprtc
-        from land_trendr_amd.index_eqn import IndexProgram
-        sc.values = None  # only the bands travel
-        torch.cuda.empty_cache()
-    meta = build_scene(sc.dates, parse_date('2014-07-01'))
+    mosaic_cfg = 'scenes' in cfg
+    if mosaic_cfg:  # one mosaic for the whole job, tiles round-robin over the ranks
+        tile = args.tile or ((P + 7) // 8 + 63) // 64 * 64
+        mosaic = Mosaic([P] * cfg['scenes'], tile, world, rank, 'round_robin')
+    else:  # one scene per rank (weak scaling)
+        tile = args.tile or (1 << 24)
+        mosaic = Mosaic([P] * world, tile, world, rank, 'by_scene')
+    items = mosaic_inputs(mosaic, cfg['years'], cfg['k'][0], cfg['k'][1], cfg['mask'],
+                          cfg['seed'], dev, TARGET)
     params, rules = compile_params(cfg['line_cost'], cfg['rules'], cfg['mode'])
     eng = get_engine(local)
-    if bands_in:
-        index_fn = eng.compile_index(IndexProgram('B1 - B2', band_dtype='int16'))
-        # the index raster of the whole scene ([K, P], like rast_algebra's per-scene output):
-        # tile views share the row stride of the cloud-mask planes (one stride per tile input)
-        index_buf = torch.empty((meta.n_obs, P), dtype=torch.int16, device=dev)
-    idx_events = []
+    index_fn = eng.compile_index(IndexProgram('B1 - B2', band_dtype='int16'))
     fields = ['status', 'matched', 'class_val', 'onset_year', 'duration', 'magnitude']
     if cfg['trendline']:
-        fields += ['winner', 'val_raw', 'val_fit', 'fit_m', 'fit_b', 'right_m', 'right_b',
-                   'spike', 'vertex']
-    gather = dist is not None and not args.no_gather
-    if args.tile <= 0:
-        # c2 sweep on one MI355X (profiles/r01_c2_tile_sweep.txt): 2 Mpx 1459, 4 Mpx 1569,
-        # 8 Mpx 1627, 16 Mpx 1647, 25 Mpx 1650, one 49 Mpx tile 1629 Mpx/s — fewer launch tails
-        args.tile = 1 << 24
-    tiles = [(p0, min(P, p0 + args.tile)) for p0 in range(0, P, args.tile)]
-    # tile-major output planes: tile t's [R|Y, tile] slab of every field is contiguous, so it can
-    # be handed to RCCL as soon as its kernels are queued
-    slabs = [eng.alloc_outputs(meta.n_years, params.n_rules, args.tile, fields) for _ in tiles]
-    recv = None
-    if gather and rank == 0:  # the writer's label rasters for the whole job, allocated once
-        recv = {f: [[torch.empty_like(sl[f]) for sl in slabs] for _ in range(world)]
-                for f in LABEL_GATHER_FIELDS}
-    works = []
-
-    # tiles per lt_analyze_tiles call: all of them, or groups whose label rasters go to RCCL
-    # while the next group computes
-    # (gathering: one tile per call, so tile t's label rasters travel while tile t+1 computes;
-    # N=1 layout proxies on one MI355X: 16.8 Mpx x 1 per call 1629, 8.4 Mpx x 2 1613, 4.19 Mpx
-    # x 4 1554 Mpx/s, profiles/r01_c2_tile_sweep.txt)
-    group = args.group if args.group > 0 else (len(tiles) if not gather else 1)
-
-    # the load stage runs on its own stream: tile t's analyze kernel waits only for tile t's
-    # index raster, so later tiles' index kernels (HBM-bound) run beside earlier tiles' analyze
-    # kernels (issue-bound) instead of all of them ahead of the first analyze
-    load_stream = torch.cuda.Stream(dev) if bands_in and not args.serial_load else None
-
-    def step(timed=False):
-        values, ready = [], []
-        main = torch.cuda.current_stream(dev)
-        if load_stream is not None:  # the previous step's analyze kernels read index_buf
-            load_stream.wait_stream(main)
-        for t, (p0, p1) in enumerate(tiles):  # the load stage: index_eqn over every tile
-            if bands_in:
-                with torch.cuda.stream(load_stream if load_stream is not None else main):
-                    e0 = e1 = None
-                    if timed:
-                        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(
-                            enable_timing=True)
-                        e0.record()
-                    values.append(eng.index_tile(index_fn, sc.bands[:, :, p0:p1],
-                                                 out=index_buf[:, p0:p1]))
-                    if timed:
-                        e1.record()
-                        idx_events.append((e0, e1))
-                    ev = None
-                    if load_stream is not None:
-                        ev = torch.cuda.Event()
-                        ev.record()
-                    ready.append(ev)
-            else:
-                values.append(sc.values[:, p0:p1])
-                ready.append(None)
-        for g0 in range(0, len(tiles), group):
-            ts = range(g0, min(len(tiles), g0 + group))
-            # analyze + label (tile t's resolve stage beside tile t+1's analyze stage)
-            eng.analyze_tiles(
-                meta, params,
-                [(values[t], sc.valid[:, tiles[t][0]:tiles[t][1]] if sc.valid is not None
-                  else None) for t in ts], fields,
-                outs=[{f: x[..., :tiles[t][1] - tiles[t][0]] for f, x in slabs[t].items()}
-                      for t in ts],
-                ready=[ready[t] for t in ts] if load_stream is not None else None)
-            if gather:  # these tiles' label rasters to the writer rank, on
-                # RCCL's stream: they travel while the next group computes
-                for t in ts:
-                    for f in LABEL_GATHER_FIELDS:
-                        works.append(dist.gather(
-                            slabs[t][f],
-                            [recv[f][r][t] for r in range(world)] if rank == 0 else None,
-                            dst=0, async_op=True))
-        while works:
-            works.pop().wait()
+        fields += TRENDLINE_FIELDS
+    runner = MosaicRunner(eng, mosaic, params, items, fields, index_fn, dist,
+                          exchange_fields=() if args.no_gather else
+                          ('class_val', 'onset_year', 'duration', 'magnitude'),
+                          load_stream=not args.serial_load, group=args.group)
+    gather = world > 1 and not args.no_gather
 
     for _ in range(args.warmup):
-        step()
+        runner.step()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -272,7 +279,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step(timed=True)
+        runner.step(timed=True)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if dist is not None:
@@ -284,72 +291,132 @@ def main():
     if dist is not None:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     elapsed = float(elapsed.item())
+    index_ms = runner.index_ms()
 
     # correctness gate on this run's own outputs: no pixel may be flagged as an unemulated path
-    n_numeric = sum(int(((sl['status'][:p1 - p0] & 16) != 0).sum().item())
-                    for sl, (p0, p1) in zip(slabs, tiles))
+    n_numeric = sum(int(((o['status'][:it.tile.n] & 16) != 0).sum().item())
+                    for o, it in zip(runner.outs, items))
+    # the load kernel alone (its HBM roofline): one tile, serially, after the timed region
+    it0 = items[0]
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    eng.index_tile(index_fn, it0.bands, out=it0.values)
+    ev[0].record()
+    for _ in range(5):
+        eng.index_tile(index_fn, it0.bands, out=it0.values)
+    ev[1].record()
+    torch.cuda.synchronize()
+    index_alone_ms = ev[0].elapsed_time(ev[1]) / 5
+    K0 = it0.scene.n_obs
+    index_bytes = K0 * it0.tile.n * 6  # two int16 band planes read, one int16 plane written
 
-    total_px = P * world * args.steps
+    e2e = None
+    if args.e2e_steps > 0:
+        if dist is not None:
+            dist.barrier()
+        dt, bh, bd = end_to_end(runner, cfg, args.e2e_steps)
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        if dist is not None:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+        e2e = {'value': round(mosaic.n_pix * args.e2e_steps / dt / 1e6, 3), 'unit': 'Mpixels/s',
+               'ms_per_step': round(dt / args.e2e_steps * 1e3, 3), 'steps': args.e2e_steps,
+               'h2d_bytes_per_step_rank0': bh // args.e2e_steps,
+               'd2h_bytes_per_step_rank0': bd // args.e2e_steps,
+               'includes': 'H2D of pinned int16 bands per tile (copy stream, overlapped), '
+                           'index_eqn, analyze, label exchange, D2H of the writer\'s label '
+                           'rasters' + (' and of every per-year trendline plane per tile '
+                                        '(TrendlineStream)' if cfg['trendline'] else '')}
+
+    total_px = mosaic.n_pix * args.steps
     value = total_px / elapsed / 1e6
     n_launch = max(1, stages['launches'])
     kern_ms = stages['analyze'] / n_launch
     resolve_ms = stages['resolve'] / n_launch
-    px_per_launch = P * args.steps / n_launch
-    flops = f_ref(cfg['years']) * px_per_launch
-    achieved = flops / (kern_ms * 1e-3) / 1e12
-    bpp = bytes_per_pixel(cfg, meta.n_obs, meta.n_years, 2 if bands_in else 8)
-    index_ms = (sum(a.elapsed_time(b) for a, b in idx_events) / max(1, len(idx_events))
-                if idx_events else None)
+    my_px = sum(it.tile.n for it in items)
+    px_per_launch = my_px * args.steps / n_launch
+    meta = items[0].scene
+    pmc = pmc_summary(args.config)
+    valu_px = per_px(pmc, 'analyze', 'SQ_INSTS_VALU')
+    achieved = (valu_px * px_per_launch / (kern_ms * 1e-3) / 1e9) if valu_px else None
+    pmc_frac = None
+    if pmc and 'GRBM_GUI_ACTIVE' in pmc.get('analyze', {}):
+        a = pmc['analyze']  # clock-free: VALU issue cycles / SIMD cycles of the PMC launch
+        pmc_frac = a['SQ_INSTS_VALU'] * CYC_PER_VALU / (SIMDS * a['GRBM_GUI_ACTIVE'] / 8)
+    step_valu = None
+    if pmc:
+        tot = sum(per_px(pmc, k, 'SQ_INSTS_VALU') or 0.0 for k in ('analyze', 'resolve', 'index'))
+        step_valu = tot * my_px * args.steps / elapsed / 1e9
+    f64_px = None
+    if pmc:
+        a = pmc.get('analyze', {})
+        if 'SQ_INSTS_VALU_FMA_F64' in a:
+            f64_px = 64 * (a['SQ_INSTS_VALU_ADD_F64'] + a['SQ_INSTS_VALU_MUL_F64'] +
+                           2 * a['SQ_INSTS_VALU_FMA_F64']) / pmc['_pixels_per_launch']
+    traffic_px = per_px(pmc, 'analyze', 'hbm_bytes')
+    bpp = bytes_per_pixel(cfg, meta.n_obs, meta.n_years)
     hbm_gbs = bpp * px_per_launch / (kern_ms * 1e-3) / 1e9
-    traffic = pmc_traffic('analyze', px_per_launch, args.input) if args.config == 'c2' else None
-    issued = (pmc_fp64_issued('analyze', px_per_launch, args.input) if args.config == 'c2'
-              else None)
+    ref_equiv = f_ref(cfg['years']) * px_per_launch / (kern_ms * 1e-3) / 1e12
+
+    def r(x, n=4):
+        return None if x is None else round(x, n)
+
     res = {
-        'metric': 'Mpixels/sec full analyze (30-yr series)' if cfg['years'] == 30 else
-                  'Mpixels/sec full analyze (%d-yr series)' % cfg['years'],
+        'metric': 'Mpixels/sec full analyze (%d-yr series)' % cfg['years'],
         'value': round(value, 4), 'unit': 'Mpixels/s', 'n_gpus': world, 'steps': args.steps,
         'warmup': args.warmup, 'ms_per_step': round(elapsed / args.steps * 1e3, 3),
-        'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f64',
-        'data': 'synthetic (SURVEY.md 8(d) generator, seeded, generated in HBM)',
-        'config': {'workload': cfg['desc'], 'pixels_per_gpu': P, 'years': cfg['years'],
+        'higher_is_better': True, 'scaling': 'strong' if mosaic_cfg else 'weak',
+        'vs_baseline': None, 'dtype': 'f64',
+        'data': 'synthetic (SURVEY.md 8(d) generator, seeded per scene, generated in HBM)',
+        'config': {'workload': cfg['desc'], 'pixels_per_scene': P, 'scenes': len(
+                       mosaic.scene_pixels), 'total_pixels': mosaic.n_pix, 'years': cfg['years'],
                    'obs': meta.n_obs, 'rules': len(rules), 'line_cost': cfg['line_cost'],
-                   'tile_pixels': args.tile, 'gather': bool(gather),
-                   'input': ('int16 bands B1, B2 + index_eqn "B1 - B2"' if bands_in else
-                             'float64 index values'),
-                   'parallelism': 'pixel tiles, 1 scene per GPU'},
-        # dominant kernel: the analyze stage, FP64-VALU bound (O(n^2) DP per 240-byte series).
-        # achieved = the reference algorithm's flops (F_ref) per launch / the
-        # launch's HIP-event time: frac > 1 means faster than the reference's own arithmetic could
-        # run at FP64 peak (the kernel proves most candidate fits irrelevant)
-        'roofline': {'bound': 'fp64-valu', 'achieved': round(achieved, 3),
-                     'peak': FP64_PEAK_TFLOPS, 'unit': 'TFLOP/s',
-                     'frac': round(achieved / FP64_PEAK_TFLOPS, 4),
-                     'traffic': None if traffic is None else round(traffic),
-                     'traffic_source': os.path.relpath(PMC_SUMMARY, ROOT) if traffic else None,
+                   'tile_pixels': tile, 'tiles': len(mosaic.tiles), 'tiles_rank0': len(items),
+                   'gather': bool(gather),
+                   'input': 'int16 bands B1, B2 + index_eqn "B1 - B2"',
+                   'parallelism': ('one mosaic, tiles round-robin over %d GPU(s), labels sent '
+                                   'to rank 0' % world) if mosaic_cfg else
+                                  ('one scene per GPU (%d), labels sent to rank 0' % world)},
+        # dominant kernel: analyze (>= 80 % of the GPU time), bound by VALU instruction issue —
+        # not HBM (85 B/px) and not FP64 throughput (22 % of its VALU work is FP64). achieved =
+        # the VALU wave-instructions it issues per launch (PMC SQ_INSTS_VALU per pixel, committed
+        # summary) x pixels per launch / the launch's live HIP-event time; peak = 1024 SIMDs x
+        # 2.4 GHz / 4 cycles per wave64 VALU instruction
+        'roofline': {'bound': 'valu-issue', 'achieved': r(achieved, 2), 'peak': VALU_PEAK_G,
+                     'unit': 'G VALU wave-instr/s',
+                     'frac': r(achieved / VALU_PEAK_G if achieved else None),
+                     'traffic': None if traffic_px is None else round(traffic_px * px_per_launch),
+                     'traffic_source': pmc['_path'] if traffic_px is not None else None,
                      'kernel': 'analyze_fast_kernel', 'kernel_ms': round(kern_ms, 3),
-                     'flops_per_px': f_ref(cfg['years']), 'flops_model': 'F_ref (SURVEY.md 8(d))',
-                     'algorithmic_bytes_per_px': bpp,
-                     'hbm': {'achieved': round(hbm_gbs, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                             'frac': round(hbm_gbs / HBM_PEAK_GBS, 4)},
-                     # what the hardware executed: FP64 VALU flops from the PMC summary / this
-                     # launch's time (the DP's integer, compare and select work is not counted)
-                     'fp64_issued': None if issued is None else {
-                         'achieved': round(issued / (kern_ms * 1e-3) / 1e12, 3),
+                     'valu_instr_per_px': r(valu_px, 2),
+                     'pmc_valu_issue_frac': r(pmc_frac),  # from the PMC launch alone, clock-free
+                     'step_valu_issue_frac': r(step_valu / VALU_PEAK_G if step_valu else None),
+                     'fp64': None if f64_px is None else {
+                         'achieved': r(f64_px * px_per_launch / (kern_ms * 1e-3) / 1e12, 3),
                          'peak': FP64_PEAK_TFLOPS, 'unit': 'TFLOP/s',
-                         'frac': round(issued / (kern_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS, 4),
-                         'source': os.path.relpath(PMC_SUMMARY, ROOT)}},
+                         'frac': r(f64_px * px_per_launch / (kern_ms * 1e-3) / 1e12 /
+                                   FP64_PEAK_TFLOPS)},
+                     'hbm': {'achieved': round(hbm_gbs, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                             'frac': r(hbm_gbs / HBM_PEAK_GBS),
+                             'algorithmic_bytes_per_px': bpp},
+                     'source': pmc['_path'] if pmc else None,
+                     # the reference algorithm's FP64 work (F_ref) per launch /
+                     # launch time: a work-equivalent speed, not a fraction of any peak (the
+                     # kernel proves most candidate fits irrelevant and never computes them)
+                     'reference_work_equivalent_tflops': round(ref_equiv, 2)},
         'status_numeric_pixels': n_numeric,
-        'load_stage': None if index_ms is None else {
-            'kernel': 'lt_index_kernel (hiprtc, index_eqn "B1 - B2", int16 bands -> int16)',
-            'ms_per_launch': round(index_ms, 3),
-            # on its own stream the index kernels share the CUs with analyze kernels, so a
-            # launch lasts longer than alone (--serial-load: 0.13 ms, 5.5 TB/s on c2)
-            'overlapped_with_analyze': load_stream is not None,
-            'hbm_gbs_algorithmic': round(meta.n_obs * 6 * px_per_launch / (index_ms * 1e-3) / 1e9,
-                                         1)},
+        'load_stage': {
+            'kernel': 'lt_index_kernel4 (hiprtc, index_eqn "B1 - B2", int16 bands -> int16)',
+            'ms_per_launch_overlapped': r(index_ms, 3),
+            'alone': {'ms': round(index_alone_ms, 4), 'pixels': it0.tile.n,
+                      'bytes': index_bytes,
+                      'achieved': round(index_bytes / (index_alone_ms * 1e-3) / 1e9, 1),
+                      'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                      'frac': round(index_bytes / (index_alone_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                                    4)}},
         'resolve_stage': {'ms_per_launch': round(resolve_ms, 3),
                           'deferred_pixels_last_tile': n_deferred_last,
-                          'last_tile_pixels': tiles[-1][1] - tiles[-1][0]},
+                          'last_tile_pixels': items[-1].tile.n},
+        'end_to_end': e2e,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res['cpu_baseline'] = cpu_baseline(cfg, args.cpu_seconds)

@@ -55,13 +55,31 @@ class LabelRule:
 
 
 def _qual(param, table):
+    """[qualifier, value] -> (LT_Q_* op, float value). A value that is not a number compares the
+    way Python 2 (the reference's interpreter) orders mixed types: any number is smaller than a
+    str/list/dict (so '2000' is NOT 2000) and larger than None. Each qualifier then has a constant
+    outcome, encoded with an op/value pair whose device comparison gives that same constant:
+    never-filters -> LT_Q_OTHER; always-rejects -> '=' NaN (onset), '>' +inf (duration, pre)."""
     if not param:
         return _abi.LT_Q_UNSET, 0.0
     q, v = param
     op = table.get(q, _abi.LT_Q_OTHER)
     if op == _abi.LT_Q_OTHER:
         return op, 0.0
-    return op, float(v)
+    if isinstance(v, (bool, int, float)):
+        return op, float(v)
+    # classes.py:190-211 drop the disturbance when `d <op'> v` holds, op' the negation of q
+    num_lt_v = v is not None  # number < v (v a str/list/...), number > v (v None)
+    rejects = {_abi.LT_Q_EQ: True,            # d != v: always true across types
+               _abi.LT_Q_LE: not num_lt_v,    # d > v
+               _abi.LT_Q_GE: num_lt_v,        # d < v
+               _abi.LT_Q_GT: num_lt_v,        # d <= v
+               _abi.LT_Q_LT: not num_lt_v}[op]  # d >= v
+    if not rejects:
+        return _abi.LT_Q_OTHER, 0.0
+    if op in (_abi.LT_Q_EQ, _abi.LT_Q_LE, _abi.LT_Q_GE):  # onset_year (an int year)
+        return _abi.LT_Q_EQ, float('nan')
+    return _abi.LT_Q_GT, float('inf')  # duration / pre_threshold: nothing is > +inf
 
 
 class TrendlinePoint:

@@ -13,14 +13,6 @@
 #pragma once
 #include "lt_pixel.h"
 
-// Diagnostic builds only (never the product): LT_ABLATE=1 skips the vertex fits, 2 the DP,
-// 3 the DP and despike's two sums, 4 the DP and the whole despike stage.
-#ifndef LT_ABLATE
-#define LT_ABLATE 0
-#endif
-#ifndef LT_SAMEKEY  // timing experiment only: every 2-point fit reads table slot 0 (wrong results)
-#define LT_SAMEKEY 0
-#endif
 // winner-pick batch: year slots whose value loads are issued together
 #ifndef LT_WB
 #define LT_WB 8
@@ -51,7 +43,7 @@ template <class GX, class GY>
 __device__ inline int lsq_lockstep(bool act, int m, GX X, GY Y, const lsq_xf* __restrict__ xtab,
                                    bool need_solution, bool need_ssr, double& slope, double& icpt,
                                    double& ssr) {
-  const int key = act ? (LT_SAMEKEY && m == 2 ? 0 : xset_key(m, X)) : 0;
+  const int key = act ? xset_key(m, X) : 0;
   const bool miss = act && key < 0;
   lsq_xf f;
   if (act && !miss) f = xtab[key];
@@ -221,11 +213,8 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
       }
       return seq;
     };
-    if constexpr (LT_ABLATE == 4) {
-      n = ok ? T : 0;
-    } else {
-    const double avg = LT_ABLATE == 3 ? 0.0 : npsum([&](int t) { return L.ys[t][lane]; }) / (double)T;
-    const double sd = LT_ABLATE == 3 ? __builtin_inf() : __builtin_sqrt(npsum([&](int t) {
+    const double avg = npsum([&](int t) { return L.ys[t][lane]; }) / (double)T;
+    const double sd = __builtin_sqrt(npsum([&](int t) {
                                        const double d = avg - L.ys[t][lane];
                                        return d * d;
                                      }) /
@@ -273,7 +262,6 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
         L.xn[n][lane] = (uint8_t)(L.year[y] - y0);
         n++;
       }
-    }
     }
   }
   const int nmax = wave_max(n);
@@ -491,7 +479,7 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
         j = a - 1;
       }
     }
-  } else if (nmax >= 1 && LT_ABLATE < 2) {
+  } else if (nmax >= 1) {
     const double c = P.line_cost;
     const double inf = __builtin_inf();
     double OPTa[MAXY + 1];  // per-lane private memory (wave-uniform indices)
@@ -708,7 +696,7 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
     const int mseg = has_next ? kb - ka + 1 : 2;
     const int kbase = has_next ? ka : 0;
     double sm = 0.0, sbv = 0.0, ssr = 0.0;
-    if (LT_ABLATE != 1 && __ballot(has_next)) {
+    if (__ballot(has_next)) {
       const int rc = lsq_lockstep(
           has_next, mseg, [&](int k) { return (int)L.xn[kbase + k][lane]; },
           [&](int k) { return (double)L.ys[kbase + k][lane]; }, xtab, true, false, sm, sbv, ssr);

@@ -1,69 +1,242 @@
-"""Multi-GPU scene analysis: pixel tiles sharded over ranks, label rasters gathered to a writer.
+"""Multi-GPU analysis of a scene mosaic: pixel tiles sharded over ranks, label rasters sent to a
+writer rank over RCCL point-to-point (xGMI), trendline planes streamed to the host per tile.
 
 Replaces the reference's MapReduce parallelism (MRLandTrendrJob.steps, mr_land_trendr_job.py:
-154-159: one reducer call per pixel key, Hadoop shuffle by pixel WKT, then a second shuffle by
-label key into output_reducer :128-152). Pixels are independent, so:
-  - the scene is cut into fixed-size pixel tiles, dealt round-robin to ranks (tile t -> rank
-    t % world: the per-pixel cost varies with masks/spikes, round-robin balances it);
-  - each rank analyses its tiles with no communication at all;
-  - the only collective is ONE gather of the per-rule label rasters (class_val, onset_year,
-    duration, magnitude) to the writer rank, over RCCL (backend "nccl") on a GPU job or gloo on
-    CPU tests. Per-year trendline planes are not gathered (54*T B/px: they stay on the rank that
-    computed them and are streamed out per tile).
-One process per GPU, torch.distributed initialised by the caller (torchrun env).
+154-159: one reducer call per pixel key after a Hadoop shuffle by pixel WKT, :83-126, then a second
+shuffle by label key into output_reducer, :128-152). Pixels are independent, so:
+
+  * a mosaic is one or more scenes (co-registered stacks, each with its own acquisition dates),
+    each cut into fixed-size pixel tiles; the tiles are dealt to ranks round-robin (tile t ->
+    rank t % world: per-pixel cost varies with masks and spikes, round-robin balances it) or, for
+    one scene per rank (the weak-scaling bench), by scene;
+  * each rank analyses its tiles with no communication at all;
+  * the only data exchange is the per-rule label rasters (class_val, onset_year, duration,
+    magnitude) of every tile to the writer rank. The writer holds them tile-major
+    ([n_tiles, R, tile], one contiguous slab per tile and field): its own tiles are analysed
+    straight into their slabs, and in round k (the k-th tile of every rank) each other rank sends
+    its slab with one point-to-point send per field, which the writer receives into the slab's
+    final place — on xGMI every peer has its own link to the writer, so the (world - 1) sends of
+    a round arrive in parallel, and no copy or padding follows. The sends are issued right after
+    the tile's kernels are queued, on RCCL's stream, so a tile's labels travel while the next
+    tile computes;
+  * per-year trendline planes (54*T B/px: 106 GB for a 49 Mpx, T = 40 scene) do not fit any one
+    GPU, so each rank streams them to pinned host memory per tile (TrendlineStream), overlapped
+    with the next tile's kernels, for its host-side writer.
+
+One process per GPU; torch.distributed is initialised by the caller (torchrun env). The same
+classes run over gloo on CPU tensors (tests/test_distributed.py).
 """
+from dataclasses import dataclass
+
 import torch
 
 LABEL_GATHER_FIELDS = ('class_val', 'onset_year', 'duration', 'magnitude')
 
 
+@dataclass(frozen=True)
+class Tile:
+    t: int        # global tile id (mosaic order)
+    scene: int    # scene index
+    p0: int       # pixel range inside the scene
+    p1: int
+    g0: int       # first pixel in mosaic order (scenes back to back)
+
+    @property
+    def n(self):
+        return self.p1 - self.p0
+
+
+class Mosaic:
+    """Scenes of `scene_pixels[s]` pixels cut into tiles of at most `tile` pixels, dealt to
+    `world` ranks. assign='round_robin': tile t -> rank t % world; 'by_scene': scene s -> rank
+    s % world (one scene per rank)."""
+
+    def __init__(self, scene_pixels, tile, world=1, rank=0, assign='round_robin'):
+        if tile <= 0 or world <= 0 or not 0 <= rank < world:
+            raise ValueError('bad tile / world / rank')
+        if assign not in ('round_robin', 'by_scene'):
+            raise ValueError('assign must be round_robin or by_scene')
+        self.scene_pixels = [int(n) for n in scene_pixels]
+        self.tile, self.world, self.rank, self.assign = int(tile), world, rank, assign
+        self.tiles = []
+        g = 0
+        for s, n in enumerate(self.scene_pixels):
+            for p0 in range(0, n, self.tile):
+                p1 = min(n, p0 + self.tile)
+                self.tiles.append(Tile(len(self.tiles), s, p0, p1, g + p0))
+            g += n
+        self.n_pix = g
+
+    def owner(self, tile):
+        return (tile.t if self.assign == 'round_robin' else tile.scene) % self.world
+
+    def tiles_of(self, rank):
+        return [t for t in self.tiles if self.owner(t) == rank]
+
+    @property
+    def mine(self):
+        return self.tiles_of(self.rank)
+
+    @property
+    def rounds(self):
+        """Exchange rounds: the largest number of tiles any rank owns."""
+        return max(len(self.tiles_of(r)) for r in range(self.world))
+
+
 def tile_ranges(n_pix, tile):
-    return [(p0, min(n_pix, p0 + tile)) for p0 in range(0, n_pix, tile)]
+    return [(t.p0, t.p1) for t in Mosaic([n_pix], tile).tiles]
 
 
 def my_tiles(n_pix, tile, world, rank):
-    """The tiles of `rank`: round-robin over the scene's tile list."""
-    return tile_ranges(n_pix, tile)[rank::world]
+    """The (p0, p1) tiles of `rank` in a one-scene mosaic: round-robin over the tile list."""
+    return [(t.p0, t.p1) for t in Mosaic([n_pix], tile, world, rank).mine]
 
 
-def analyze_shard(n_pix, tile, world, rank, analyze_tile_fn):
-    """Run analyze_tile_fn(p0, p1) -> {field: [R|Y, p1-p0] tensor} on this rank's tiles.
-    Returns [(p0, p1, outputs), ...] in tile order."""
-    return [(p0, p1, analyze_tile_fn(p0, p1)) for p0, p1 in my_tiles(n_pix, tile, world, rank)]
+class LabelExchange:
+    """The mosaic's label rasters on the writer rank `dst`, filled by point-to-point sends.
 
+    slab(tile) -> {field: [R, tile] tensor} is where this rank's kernels write tile `tile`'s
+    label planes (its final place on the writer, a send buffer elsewhere). post(k) queues round
+    k's sends / receives (non-blocking; on NCCL they run on RCCL's stream after the work already
+    queued on the current stream), wait() completes every posted one, raster(field) assembles
+    the writer's [R, n_pix] raster in mosaic pixel order."""
 
-def gather_labels(shard, n_pix, tile, n_rules, world, rank, dist, dst=0,
-                  fields=LABEL_GATHER_FIELDS, device=None):
-    """Gather this rank's label planes to `dst` and assemble full [n_rules, n_pix] rasters there.
+    def __init__(self, mosaic, spec, device, dist=None, dst=0):
+        """spec: {field: (rows, torch dtype)}, rows None for a [tile] plane (status) or the
+        plane count of a [rows, tile] field (R for label fields, Y for trendline fields)."""
+        self.m, self.dist, self.dst = mosaic, dist, dst
+        self.spec = dict(spec)
+        self.fields = tuple(self.spec)
+        self.device = torch.device(device)
+        self.is_writer = mosaic.rank == dst
+        T, W = len(mosaic.tiles), mosaic.tile
+        if mosaic.world > 1 and dist is None:
+            raise ValueError('world > 1 needs torch.distributed')
 
-    Each rank packs its tiles back to back into one buffer per field (padded to the largest
-    rank's pixel count), so the exchange is a single gather per field — on xGMI every peer has a
-    direct link to the writer, so the writer's ingress runs all peers in parallel."""
-    counts = [sum(p1 - p0 for p0, p1 in my_tiles(n_pix, tile, world, r)) for r in range(world)]
-    cap = max(counts) if counts else 0
-    out = {}
-    for f in fields:
-        ref = shard[0][2][f] if shard else None
-        dtype = ref.dtype if ref is not None else (torch.float64 if f == 'magnitude'
-                                                   else torch.int32)
-        dev = ref.device if ref is not None else device
-        buf = torch.zeros((n_rules, cap), dtype=dtype, device=dev)
-        off = 0
-        for p0, p1, o in shard:
-            buf[:, off:off + (p1 - p0)] = o[f][:n_rules, :p1 - p0]
-            off += p1 - p0
-        bufs = [torch.empty_like(buf) for _ in range(world)] if rank == dst else None
-        if world > 1:
-            dist.gather(buf, bufs, dst=dst)
+        def shape(f, lead=()):
+            rows = self.spec[f][0]
+            return lead + ((W,) if rows is None else (rows, W))
+
+        self.full = None
+        if self.is_writer:  # tile-major: slab t of every field is contiguous
+            self.full = {f: torch.empty(shape(f, (T,)), dtype=self.spec[f][1], device=self.device)
+                         for f in self.fields}
+            self._slabs = {t.t: {f: self.full[f][t.t] for f in self.fields} for t in mosaic.mine}
         else:
-            bufs = [buf]
-        if rank != dst:
-            continue
-        full = torch.empty((n_rules, n_pix), dtype=dtype, device=dev)
-        for r in range(world):
-            off = 0
-            for p0, p1 in my_tiles(n_pix, tile, world, r):
-                full[:, p0:p1] = bufs[r][:, off:off + (p1 - p0)]
-                off += p1 - p0
-        out[f] = full
-    return out
+            self._slabs = {t.t: {f: torch.empty(shape(f), dtype=self.spec[f][1],
+                                                device=self.device) for f in self.fields}
+                           for t in mosaic.mine}
+        # the writer's receives wait for nothing it computes: they are posted from a stream of
+        # their own (an RCCL op first waits for the work queued on the current stream)
+        self._recv_stream = (torch.cuda.Stream(self.device)
+                             if self.is_writer and self.device.type == 'cuda' else None)
+        self._works = []
+
+    def slab(self, tile):
+        return self._slabs[tile.t]
+
+    def post(self, k):
+        """Round k: the k-th tile of every rank goes to the writer."""
+        if self.m.world == 1:
+            return
+        d = self.dist
+        ops = []
+        if self.is_writer:
+            for r in range(self.m.world):
+                if r == self.dst:
+                    continue
+                mine = self.m.tiles_of(r)
+                if k < len(mine):
+                    t = mine[k].t
+                    ops += [d.P2POp(d.irecv, self.full[f][t], r) for f in self.fields]
+        else:
+            mine = self.m.mine
+            if k < len(mine):
+                s = self._slabs[mine[k].t]
+                ops += [d.P2POp(d.isend, s[f], self.dst) for f in self.fields]
+        if ops:
+            if self._recv_stream is not None:
+                with torch.cuda.stream(self._recv_stream):
+                    self._works += d.batch_isend_irecv(ops)
+            else:
+                self._works += d.batch_isend_irecv(ops)
+
+    def post_all(self):
+        for k in range(self.m.rounds):
+            self.post(k)
+
+    def wait(self):
+        while self._works:
+            self._works.pop(0).wait()
+
+    def raster(self, field):
+        """[rows, n_pix] (or [n_pix]) in mosaic pixel order (writer only): the tile-major slabs
+        laid side by side."""
+        if not self.is_writer:
+            raise ValueError('only the writer rank holds the rasters')
+        a = self.full[field]
+        out = torch.empty(a.shape[1:-1] + (self.m.n_pix,), dtype=a.dtype, device=a.device)
+        for t in self.m.tiles:
+            out[..., t.g0:t.g0 + t.n] = a[t.t, ..., :t.n]
+        return out
+
+
+class TrendlineStream:
+    """D2H of per-year trendline planes into a ring of pinned host buffers, on a copy stream.
+
+    A tile's [Y, tile] planes are copied one row (one year plane, contiguous) at a time into the
+    next ring buffer; a buffer is reused once its previous copy has completed (the host writer
+    reads it in between: `sink(field, row, host_view)` is called for each completed row when its
+    buffer comes round again, and for the rest by drain()). The copy stream waits for the work
+    queued on the current stream when push() is called, so queue tile t + 1's kernels before
+    pushing tile t: its copies then overlap them, and a push that blocks on the ring does not
+    hold back the next tile's launches."""
+
+    def __init__(self, row_bytes, device, depth=8, sink=None):
+        self.device = torch.device(device)
+        self.stream = torch.cuda.Stream(self.device)
+        self.ring = [torch.empty(int(row_bytes), dtype=torch.uint8, pin_memory=True)
+                     for _ in range(depth)]
+        self.pending = [None] * depth  # (event, field, row, nbytes) of the buffer's last copy
+        self.sink = sink
+        self.count = 0
+        self.bytes = 0
+
+    def _retire(self, slot):
+        p = self.pending[slot]
+        if p is None:
+            return
+        ev, f, row, nb = p
+        ev.synchronize()
+        if self.sink is not None:
+            self.sink(f, row, self.ring[slot][:nb])
+        self.pending[slot] = None
+
+    def push(self, planes, n=None):
+        """Queue the D2H of every row of planes[f] ([rows, W] device tensors; the first n pixels
+        of each row, all W by default) after the work queued so far on the current stream."""
+        ready = torch.cuda.Event()
+        ready.record()
+        self.stream.wait_event(ready)
+        for f, t in planes.items():
+            rows = t if t.dim() == 2 else t[None]
+            w = rows.shape[1] if n is None else n
+            for r in range(rows.shape[0]):
+                src = rows[r, :w]
+                nb = src.numel() * src.element_size()
+                slot = self.count % len(self.ring)
+                self._retire(slot)
+                dst = self.ring[slot][:nb]
+                if nb > self.ring[slot].numel():
+                    raise ValueError('row of %d bytes exceeds the ring buffers' % nb)
+                with torch.cuda.stream(self.stream):
+                    dst.copy_(src.view(torch.uint8), non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record()
+                self.pending[slot] = (ev, f, r, nb)
+                self.count += 1
+                self.bytes += nb
+
+    def drain(self):
+        for k in range(len(self.ring)):
+            self._retire((self.count + k) % len(self.ring))

@@ -243,12 +243,42 @@ def label_tile(engine, years, params, val_fit, vertex, present=None, out=None, s
     """change_labeling alone on trendlines in device memory: val_fit float64 [Y, P],
     vertex / present uint8 [Y, P] (same strides). Returns the rule-plane dict + status."""
     import numpy as np
+    # the C ABI reads val_fit, vertex and present with the one lin.stride: check every plane the
+    # way _tile_structs checks a tile (a mismatch would be an out-of-bounds device read)
+    if (not isinstance(val_fit, torch.Tensor) or val_fit.dim() != 2 or
+            val_fit.dtype != torch.float64 or val_fit.device != engine.device or
+            val_fit.stride(1) != 1):
+        raise LtError('val_fit must be a float64 [Y, P] tensor on %s with unit pixel stride'
+                      % engine.device)
+    for name, t in (('vertex', vertex), ('present', present)):
+        if t is None and name == 'present':
+            continue
+        if (not isinstance(t, torch.Tensor) or t.dtype != torch.uint8 or
+                t.device != engine.device or t.shape != val_fit.shape or
+                t.stride() != val_fit.stride()):
+            raise LtError('%s must be uint8 with the shape and strides of val_fit' % name)
     Y, P = val_fit.shape
     yrs = np.ascontiguousarray(np.asarray(years, np.int32))
     if len(yrs) != Y:
         raise LtError('years must have one entry per slot')
     if out is None:
         out = engine.alloc_outputs(Y, params.n_rules, P, LABELS + ('status',))
+    need = set(LABELS) | {'status'}
+    if not need <= set(out):
+        raise LtError('out lacks %s' % sorted(need - set(out)))
+    rstride = None
+    for f, t in out.items():
+        kind = _SHAPE_KIND.get(f)
+        if kind is None or t.device != engine.device or t.dtype != _DTYPE[f] or t.shape[-1] < P:
+            raise LtError('output %s has wrong device/dtype/shape' % f)
+        if kind == 'rule':
+            if t.dim() != 2 or t.shape[0] < max(params.n_rules, 1) or t.stride(1) != 1:
+                raise LtError('output %s too small' % f)
+            if rstride is not None and t.stride(0) != rstride:
+                raise LtError('all [R, P] outputs must share one row stride')
+            rstride = t.stride(0)
+        elif kind == 'pix' and t.stride(0) != 1:
+            raise LtError('output %s must have unit pixel stride' % f)
     lin = _abi.LtLabelIn()
     lin.n_pix = P
     lin.stride = val_fit.stride(0)
@@ -258,7 +288,7 @@ def label_tile(engine, years, params, val_fit, vertex, present=None, out=None, s
     lin.vertex = ctypes.cast(vertex.data_ptr(), _abi.c_u8p)
     lin.present = ctypes.cast(present.data_ptr(), _abi.c_u8p) if present is not None else None
     tout = _abi.LtTileOut()
-    tout.stride = out['matched'].stride(0)
+    tout.stride = rstride
     for f, t in out.items():
         setattr(tout, f, ctypes.cast(t.data_ptr(), type(getattr(tout, f))))
     st = stream if stream is not None else torch.cuda.current_stream(engine.device)

@@ -12,7 +12,9 @@ Steps, as the reference chains them:
   1. setup    (setup_mapper :20-45)   analysis rasters by RAST_TRIGGER, grid from the first one;
   2. parse    (parse_mapper :47-81)   ingest.ingest_stack: band samples + mask validity per grid
                                       point (index_eqn runs on the GPU in step 3);
-  3. analysis (analysis_reducer :83-126) utils.analysis_reducer_batch over pixel tiles on the GPU;
+  3. analysis (analysis_reducer :83-126) the mosaic path of runner.py over pixel tiles on the GPU
+                                      (tiles round-robin over the torchrun ranks, every output
+                                      plane sent to rank 0);
   4. output   (output_reducer :128-152) raster.label_rasters / trendline_rasters placed by each
                                       grid point's template offsets, written as GeoTIFFs.
 
@@ -21,6 +23,7 @@ same exception type (on_error='raise'); on_error='skip' leaves such pixels NODAT
 Grid points with no observation at all never reach the reference's reducer; they stay NODATA.
 
 CLI: python -m land_trendr_amd.job --root DIR --job NAME [--tile-pixels N] [--no-trendline]
+     (multi-GPU: torchrun --nproc-per-node N -m land_trendr_amd.job ...)
 """
 import argparse
 import json
@@ -88,33 +91,55 @@ class LocalJob:
         self.stack = ingest_stack(self.rast_fns, self.grid_fn, self.mask_fns, bands=eqn_bands)
         return self.stack
 
-    # 3. analysis_reducer, batched over pixel tiles
+    # 3. analysis_reducer, batched over pixel tiles: the mosaic path (runner.py) bench.py runs
     def analyze(self):
+        """Tiles of the grid dealt round-robin over the torch.distributed ranks (one when not
+        initialised), analysed by runner.MosaicRunner; every output plane goes to rank 0 (the
+        writer) through the LabelExchange. Returns the host planes on rank 0, None elsewhere."""
         import torch
-        from .engine import LABELS, TRENDLINE
-        from .utils import analysis_reducer_batch
+        from .distributed import Mosaic
+        from .engine import LABELS, TRENDLINE, get_engine
+        from .index_eqn import IndexProgram
+        from .runner import MosaicRunner, TileInput
+        from .scene import build_scene, parse_date
+        from .settings import compile_params
         st = self.stack
         P = st['n_pix']
-        fields = LABELS + ('status', 'n_years') + (TRENDLINE if self.trendline else ('winner',))
+        dist, world, rank = None, 1, 0
+        if torch.distributed.is_available() and torch.distributed.is_initialized():
+            dist = torch.distributed
+            world, rank = dist.get_world_size(), dist.get_rank()
         dev = torch.device('cuda', self.device if self.device is not None else
                            torch.cuda.current_device())
-        host = None
-        for p0 in range(0, P, self.tile_pixels):
-            p1 = min(P, p0 + self.tile_pixels)
-            bands = torch.from_numpy(np.ascontiguousarray(st['bands'][:, :, p0:p1])).to(dev)
-            valid = torch.from_numpy(np.ascontiguousarray(st['valid'][:, p0:p1])).to(dev)
-            out = analysis_reducer_batch(st['dates'], None, valid, self.settings, fields,
-                                         self.pre_threshold_mode, device=dev, bands=bands,
-                                         band_numbers=st['band_numbers'])
-            self.scene, self.rules = out.pop('_scene'), out.pop('_rules')
-            if host is None:
-                host = {k: np.empty(t.shape[:-1] + (P,), t.cpu().numpy().dtype)
-                        for k, t in out.items()}
-            for k, t in out.items():
-                host[k][..., p0:p1] = t.cpu().numpy()
-        self.planes = host
+        fields = LABELS + ('status', 'n_years') + (TRENDLINE if self.trendline else ('winner',))
+        self.scene = build_scene(st['dates'], parse_date(self.settings['target_date']))
+        params, self.rules = compile_params(self.settings['line_cost'],
+                                            self.settings.get('label_rules', ()),
+                                            self.pre_threshold_mode)
+        eng = get_engine(dev)
+        numbers = list(st['band_numbers'])
+        prog = IndexProgram(self.settings['index_eqn'], band_dtype=st['bands'].dtype,
+                            raster_count=max(numbers))
+        slots = [numbers.index(b) for b in prog.bands]  # the planes the equation reads
+        fn = eng.compile_index(prog)
+        m = Mosaic([P], self.tile_pixels, world, rank, 'round_robin')
+        K = self.scene.n_obs
+        items = []
+        for t in m.mine:
+            bands = torch.from_numpy(np.ascontiguousarray(
+                st['bands'][:, slots, t.p0:t.p1])).to(dev)
+            valid = torch.from_numpy(np.ascontiguousarray(st['valid'][:, t.p0:t.p1])).to(dev)
+            vals = torch.empty((K, t.n), dtype=bands.dtype, device=dev)
+            items.append(TileInput(t, self.scene, vals, valid, bands))
+        runner = MosaicRunner(eng, m, params, items, fields, fn, dist, exchange_fields=fields)
+        runner.step()
+        torch.cuda.synchronize(dev)
+        if not runner.exchange.is_writer:
+            self.planes = None
+            return None
+        self.planes = {f: runner.exchange.raster(f).cpu().numpy() for f in fields}
         self._check_errors()
-        return host
+        return self.planes
 
     def _check_errors(self):
         from .utils import _raise_for_status
@@ -169,9 +194,12 @@ class LocalJob:
         return dict(output_reducer(rasters, tmpl, self.root, self.job))
 
     def run(self):
+        """Every rank runs setup/parse/analysis; the writer (rank 0) also writes the rasters.
+        Returns {key: [path]} on the writer, None on the other ranks."""
         self.setup()
         self.parse()
-        self.analyze()
+        if self.analyze() is None:
+            return None
         return self.output()
 
 
@@ -188,11 +216,22 @@ def main(argv=None):
                     default='reference')
     ap.add_argument('--on-error', choices=('raise', 'skip'), default='raise')
     a = ap.parse_args(argv)
+    dist = None
+    if int(os.environ.get('WORLD_SIZE', '1')) > 1:
+        import torch
+        import torch.distributed as dist
+        local = int(os.environ.get('LOCAL_RANK', '0'))
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        if a.device is None:
+            a.device = local
     j = LocalJob(a.root, a.job, a.device, a.tile_pixels, not a.no_trendline, a.raster_mode,
                  a.pre_threshold_mode, a.on_error)
     res = j.run()
-    for key in sorted(res):
+    for key in sorted(res or {}):
         print('%s\t%s' % (key, res[key][0]))
+    if dist is not None:
+        dist.destroy_process_group()
     return 0
 
 

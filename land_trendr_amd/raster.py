@@ -36,6 +36,15 @@ _PLANE_OF_ATTR = {'val_raw': 'val_raw', 'val_fit': 'val_fit', 'eqn_fit_slope': '
                   'eqn_right_intercept': 'right_b', 'spike': 'spike', 'vertex': 'vertex'}
 
 
+def holder_dtype(template_dtype):
+    """dtype of the reference's holder `np.ones_like(template) * NODATA` (utils.py:429) under
+    numpy 1.x value-based promotion: the template's own type when it holds -99 (int16 -> int16,
+    float32 -> float32), else the smallest signed type that does (uint8 -> int16,
+    uint16 -> int32, uint32 -> int64)."""
+    from .index_eqn import result_dtype
+    return result_dtype(np.dtype(template_dtype), NODATA)
+
+
 def _holder_cast(values, template_dtype):
     """numpy's assignment of float(value) into the holder's dtype (utils.py:433-438)."""
     v = np.asarray(values, np.float64)
@@ -71,8 +80,9 @@ def label_rasters(out, rules, shape, template_dtype=np.int16, mode='reference'):
                 typ = np.float64 if key == 'magnitude' else np.int32
                 res['%s_%s' % (rule.name, key)] = np.where(m, plane, NODATA).astype(typ)
             else:
-                holder = np.full((rows, cols), NODATA, np.int64).astype(template_dtype)
-                holder[m] = _holder_cast(plane[m], template_dtype)
+                hdt = holder_dtype(template_dtype)
+                holder = np.full((rows, cols), NODATA, hdt)
+                holder[m] = _holder_cast(plane[m], hdt)
                 res['%s_%s' % (rule.name, key)] = gdal_to_byte(holder)
     return res
 
@@ -103,8 +113,9 @@ def trendline_rasters(out, scene, dates, shape, template_dtype=np.int16, mode='r
                     res[key] = r.astype(typ) if typ != np.uint8 else np.where(sel, plane, 0).astype(
                         np.uint8)
                 else:
-                    holder = np.full((rows, cols), NODATA, np.int64).astype(template_dtype)
-                    holder[sel] = _holder_cast(plane[sel], template_dtype)
+                    hdt = holder_dtype(template_dtype)
+                    holder = np.full((rows, cols), NODATA, hdt)
+                    holder[sel] = _holder_cast(plane[sel], hdt)
                     res[key] = gdal_to_byte(holder)
     return res
 

@@ -1,0 +1,148 @@
+"""The per-rank tile pipeline of a mosaic job: load stage -> analyze + label -> label exchange.
+
+For every tile this rank owns (distributed.Mosaic), in tile order:
+  1. load stage (parse_mapper's rast_algebra, mr_land_trendr_job.py:67-68 / utils.py:447-484):
+     the hiprtc-compiled index_eqn kernel turns the tile's band planes into its index raster, on a
+     stream of its own, recording an event per tile;
+  2. analyze + label (analysis_reducer, mr_land_trendr_job.py:83-126): lt_analyze_tiles_after on
+     the current stream, tile t waiting only for tile t's index event, so later tiles' load
+     kernels (HBM-bound) run beside earlier tiles' analyze kernels (issue-bound); consecutive
+     tiles of one scene share a call (tile t's resolve stage runs beside tile t+1's analyze);
+  3. the tile's label rasters go to the writer rank (distributed.LabelExchange) as soon as its
+     kernels are queued, so they travel while the next tile computes.
+bench.py, the job runner (job.py) and the GPU tests all run this one code path.
+"""
+import contextlib
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+
+from .distributed import LABEL_GATHER_FIELDS, LabelExchange
+from .engine import _DTYPE, _SHAPE_KIND
+
+
+_nullctx = contextlib.nullcontext
+
+
+@dataclass
+class TileInput:
+    tile: object                       # distributed.Tile
+    scene: object                      # scene.SceneMeta (lt_scene of the tile's scene)
+    values: torch.Tensor               # [K, n] index raster (written by the load stage if bands)
+    valid: Optional[torch.Tensor]      # [K, n] uint8 or None
+    bands: Optional[torch.Tensor] = None  # [K, NB, n] band planes, or None (values given)
+
+
+class MosaicRunner:
+    """One rank's share of a mosaic job on one GPU.
+
+    fields: the output planes the kernels write per tile; label fields in `exchange_fields` live
+    in the LabelExchange's slabs (their final place on the writer rank), the others in per-tile
+    slabs of this rank. group: tiles per lt_analyze_tiles call (0: every consecutive tile of a
+    scene, or 1 when labels are exchanged, so tile t's sends travel while tile t+1 computes)."""
+
+    def __init__(self, engine, mosaic, params, items, fields, index_fn=None, dist=None,
+                 exchange_fields=LABEL_GATHER_FIELDS, load_stream=True, group=0, dst=0):
+        self.eng, self.m, self.params, self.items = engine, mosaic, params, list(items)
+        self.fields = tuple(fields)
+        self.index_fn = index_fn
+        if [it.tile.t for it in self.items] != [t.t for t in mosaic.mine]:
+            raise ValueError('items must be this rank\'s tiles, in mosaic order')
+        R = max(params.n_rules, 1)
+        ys = {it.scene.n_years for it in self.items} or {0}
+        Y = max(ys)
+        ex = [f for f in exchange_fields if f in self.fields]
+
+        def rows(f):
+            k = _SHAPE_KIND[f]
+            return None if k == 'pix' else (R if k == 'rule' else Y)
+
+        self.exchange = LabelExchange(mosaic, {f: (rows(f), _DTYPE[f]) for f in ex},
+                                      engine.device, dist, dst)
+        W = mosaic.tile
+        self.outs = []
+        for it in self.items:
+            o = dict(self.exchange.slab(it.tile))
+            for f in self.fields:
+                if f not in o:
+                    r = rows(f)
+                    o[f] = torch.empty((W,) if r is None else (r, W), dtype=_DTYPE[f],
+                                       device=engine.device)
+            self.outs.append(o)
+        gathering = mosaic.world > 1 and bool(ex)
+        self.group = group if group > 0 else (1 if gathering else 1 << 30)
+        has_bands = any(it.bands is not None for it in self.items)
+        if has_bands and index_fn is None:
+            raise ValueError('band inputs need a compiled index_eqn (index_fn)')
+        # (a CPU engine — the gloo tests' oracle double — has no streams: everything is serial)
+        self.cuda = torch.device(engine.device).type == 'cuda'
+        self.load_stream = (torch.cuda.Stream(engine.device)
+                            if self.cuda and has_bands and load_stream else None)
+        self.index_events = []  # (start, stop) pairs of the timed steps' load kernels
+
+    def _groups(self):
+        """Consecutive items of one scene, at most self.group per call."""
+        g = []
+        for k, it in enumerate(self.items):
+            if g and (it.tile.scene != self.items[g[0]].tile.scene or len(g) >= self.group):
+                yield g
+                g = []
+            g.append(k)
+        if g:
+            yield g
+
+    def step(self, timed=False, after_tile=None, stage_in=None):
+        """Queue one pass over this rank's tiles and complete the label exchange.
+        after_tile(k): called once tile k's kernels are queued (e.g. to stream its trendline).
+        stage_in: an object whose fetch(k) -> (bands, event) supplies tile k's band planes from
+        elsewhere (an H2D copy the load kernel waits for) and whose consumed(k, event) learns
+        when the load kernel has read them."""
+        eng = self.eng
+        if not self.cuda:
+            timed = False
+        main = torch.cuda.current_stream(eng.device) if self.cuda else None
+        ready = [None] * len(self.items)
+        if self.load_stream is not None:  # the previous step's analyze kernels read the rasters
+            self.load_stream.wait_stream(main)
+        for k, it in enumerate(self.items):
+            if it.bands is None:
+                continue
+            bands = it.bands
+            if stage_in is not None:
+                bands, ev_in = stage_in.fetch(k)
+            with (torch.cuda.stream(self.load_stream if self.load_stream is not None else main)
+                  if self.cuda else _nullctx()):
+                if stage_in is not None:
+                    torch.cuda.current_stream(eng.device).wait_event(ev_in)
+                if timed:
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(
+                        enable_timing=True)
+                    e0.record()
+                eng.index_tile(self.index_fn, bands, out=it.values)
+                if timed:
+                    e1.record()
+                    self.index_events.append((e0, e1))
+                if self.cuda and (self.load_stream is not None or stage_in is not None):
+                    ev = torch.cuda.Event()
+                    ev.record()
+                    ready[k] = ev
+                    if stage_in is not None:
+                        stage_in.consumed(k, ev)
+        for g in self._groups():
+            scene = self.items[g[0]].scene
+            n = [self.items[k].tile.n for k in g]
+            eng.analyze_tiles(
+                scene, self.params, [(self.items[k].values, self.items[k].valid) for k in g],
+                self.fields, outs=[{f: x[..., :nk] for f, x in self.outs[k].items()}
+                                   for k, nk in zip(g, n)],
+                ready=[ready[k] for k in g] if self.load_stream is not None else None)
+            for k in g:
+                self.exchange.post(k)
+                if after_tile is not None:
+                    after_tile(k)
+        self.exchange.wait()
+
+    def index_ms(self):
+        ev, self.index_events = self.index_events, []
+        return sum(a.elapsed_time(b) for a, b in ev) / len(ev) if ev else None

@@ -87,3 +87,39 @@ def make_scene(n_pix, n_years=30, k_min=1, k_max=1, mask_prob=0.0, first_year=19
     return Scene(dates=dates, values=values, valid=valid, bands=bands,
                  meta=dict(n_years=n_years, k_min=k_min, k_max=k_max, mask_prob=mask_prob,
                            first_year=first_year, seed=seed))
+
+
+def mosaic_inputs(mosaic, n_years, k_min=1, k_max=1, mask_prob=0.0, seed0=1000, device='cpu',
+                  target_date='2014-07-01'):
+    """runner.TileInput for every tile this rank owns in `mosaic`: scene s is the seeded scene
+    make_scene(seed=seed0 + s) as int16 bands (B1, B2) + cloud mask, so a tile's content does not
+    depend on the number of ranks. A rank owning a whole scene keeps it in place (tiles are views
+    sharing one index raster); otherwise its tiles are copied out and the scene freed."""
+    from .runner import TileInput
+    from .scene import build_scene, parse_date
+    items = []
+    dev = torch.device(device)
+    for s in sorted({t.scene for t in mosaic.mine}):
+        sc = make_scene(mosaic.scene_pixels[s], n_years=n_years, k_min=k_min, k_max=k_max,
+                        mask_prob=mask_prob, seed=seed0 + s, device=dev, with_bands=True)
+        sc.values = None  # only the bands travel (the load stage computes the index raster)
+        meta = build_scene(sc.dates, parse_date(target_date))
+        mine = [t for t in mosaic.mine if t.scene == s]
+        whole = len(mine) == sum(1 for t in mosaic.tiles if t.scene == s)
+        K, P = meta.n_obs, mosaic.scene_pixels[s]
+        index = torch.empty((K, P), dtype=torch.int16, device=dev) if whole else None
+        for t in mine:
+            sl = slice(t.p0, t.p1)
+            if whole:
+                items.append(TileInput(t, meta, index[:, sl],
+                                       sc.valid[:, sl] if sc.valid is not None else None,
+                                       sc.bands[:, :, sl]))
+            else:
+                items.append(TileInput(t, meta, torch.empty((K, t.n), dtype=torch.int16,
+                                                            device=dev),
+                                       sc.valid[:, sl].clone() if sc.valid is not None else None,
+                                       sc.bands[:, :, sl].clone()))
+        del sc
+        if dev.type == 'cuda':
+            torch.cuda.empty_cache()
+    return items

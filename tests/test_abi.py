@@ -106,6 +106,32 @@ def test_rule_compilation():
     assert (r[2].change_type, r[2].duration_op) == (3, _abi.LT_Q_UNSET)
 
 
+def test_non_numeric_qualifiers_follow_python2_ordering():
+    """The reference runs on Python 2, where a number compares below any str/list and above None
+    (classes.py:190-211 compare the raw JSON value): '2000' is not 2000. Each such qualifier has
+    a constant outcome; the compiled rules reproduce it (checked through the oracle's labels)."""
+    from land_trendr_amd.synth import make_scene
+    from oracle import oracle
+    sc = make_scene(256, n_years=30, seed=9)
+    meta = build_scene(sc.dates, parse_date('2014-07-01'))
+    base = {'name': 'g', 'val': 1, 'change_type': 'GD'}
+    cases = [  # (filter, same-as-unfiltered?)
+        ({'onset_year': ['>=', '2000']}, False), ({'onset_year': ['<=', '2000']}, True),
+        ({'onset_year': ['=', '1990']}, False), ({'onset_year': ['<=', None]}, False),
+        ({'onset_year': ['>=', None]}, True), ({'duration': ['>', 'x']}, False),
+        ({'duration': ['<', 'x']}, True), ({'duration': ['>', None]}, True),
+        ({'duration': ['<', None]}, False), ({'onset_year': ['>=', [1]]}, False),
+        ({'pre_threshold': ['>', 'x']}, False), ({'pre_threshold': ['<', 'x']}, True),
+    ]
+    params, _ = compile_params(10.0, [base] + [dict(base, name='r%d' % i, **f)
+                                               for i, (f, _) in enumerate(cases)], 'documented')
+    out = oracle.analyze_tile(meta, params, sc.values.numpy(), None)
+    m = out['matched']
+    assert m[0].sum() > 200
+    for i, (f, same) in enumerate(cases):
+        assert (m[i + 1] == m[0]).all() if same else not m[i + 1].any(), f
+
+
 # ---- pick_winners' date half (utils.py:491-521) ----
 
 def test_scene_grouping_and_distances():

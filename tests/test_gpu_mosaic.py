@@ -1,0 +1,153 @@
+"""The bench / job code path on the GPU at BASELINE.json sizes: synthetic int16 band stacks
+(synth.mosaic_inputs, bench.py's seeds and tiling) -> index_eqn 'B1 - B2' on the load stream ->
+lt_analyze_tiles_after -> label exchange (runner.MosaicRunner), checked against the CPU oracle on
+200,000 sampled pixels per config (fed the index raster the load kernel wrote, as the reference's
+apply_grid feeds float(val) of the rast_algebra raster), plus whole-raster invariants. c4 is the
+4-scene, 196 Mpx mosaic of configs[3], dealt round-robin in 6.1 Mpx tiles as bench.py deals it
+(one rank here: every tile of the mosaic on this GPU)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import bench
+from land_trendr_amd.distributed import Mosaic, TrendlineStream
+from land_trendr_amd.engine import get_engine
+from land_trendr_amd.index_eqn import IndexProgram
+from land_trendr_amd.runner import MosaicRunner
+from land_trendr_amd.settings import compile_params
+from land_trendr_amd.synth import mosaic_inputs
+
+pytestmark = pytest.mark.gpu
+SAMPLE = 200_000
+
+
+def _threads():
+    try:
+        return min(len(os.sched_getaffinity(0)), 64)
+    except AttributeError:
+        return 8
+
+
+def _same(a, b):
+    if a.dtype.kind == 'f':
+        return (a.view(np.int64) == b.view(np.int64)) | (np.isnan(a) & np.isnan(b))
+    return a == b
+
+
+def _bench_runner(cfg_name, fields, pixels=0):
+    c = bench.CONFIGS[cfg_name]
+    P = pixels or c['pixels']
+    if 'scenes' in c:
+        tile = ((P + 7) // 8 + 63) // 64 * 64
+        m = Mosaic([P] * c['scenes'], tile, 1, 0, 'round_robin')
+    else:
+        m = Mosaic([P], 1 << 24, 1, 0, 'by_scene')
+    eng = get_engine(0)
+    items = mosaic_inputs(m, c['years'], c['k'][0], c['k'][1], c['mask'], c['seed'],
+                          eng.device, bench.TARGET)
+    params, _ = compile_params(c['line_cost'], c['rules'], c['mode'])
+    fn = eng.compile_index(IndexProgram('B1 - B2', band_dtype='int16'))
+    return MosaicRunner(eng, m, params, items, fields, fn), params
+
+
+@pytest.mark.parametrize('cfg', ['c2', 'c3', 'c4', 'c5'])
+def test_bench_path_full_size_sampled_vs_oracle(cfg):
+    from oracle import oracle
+    c = bench.CONFIGS[cfg]
+    fields = ['status', 'matched', 'class_val', 'onset_year', 'duration', 'magnitude']
+    if cfg == 'c5':
+        fields += bench.TRENDLINE_FIELDS
+    elif cfg != 'c4':
+        fields += ['val_fit', 'vertex']
+    runner, params = _bench_runner(cfg, fields)
+    runner.step()
+    torch.cuda.synchronize()
+    m = runner.m
+    rng = np.random.default_rng(11)
+    n_checked = 0
+    for s in range(len(m.scene_pixels)):  # per scene: invariants, then a sample vs the oracle
+        items = [(k, it) for k, it in enumerate(runner.items) if it.tile.scene == s]
+        for k, it in items:
+            o = {f: t[..., :it.tile.n] for f, t in runner.outs[k].items()}
+            assert int((o['status'] != 0).sum()) == 0, (cfg, it.tile)
+            mt = o['matched'].bool()
+            assert bool(((o['class_val'] != -99) == mt).all())
+            assert bool(((o['duration'] > 0) | ~mt).all())
+            # the load stage: the index raster is B1 - B2 of the tile's int16 bands
+            b = it.bands
+            assert torch.equal(it.values, (b[:, 0, :].int() - b[:, 1, :].int()).short())
+        n = SAMPLE // len(m.scene_pixels)
+        for k, it in items:
+            share = max(1, n * it.tile.n // m.scene_pixels[s])
+            idx = torch.from_numpy(np.sort(rng.choice(it.tile.n, share, replace=False))).to(
+                it.values.device)
+            vals = it.values[:, idx].double().cpu().numpy()
+            valid = it.valid[:, idx].cpu().numpy() if it.valid is not None else None
+            want = oracle.analyze_tile(it.scene, params, vals, valid, n_threads=_threads())
+            for f in fields:
+                a = want[f]
+                g = runner.outs[k][f][..., idx].cpu().numpy()
+                same = _same(a[:g.shape[0]] if a.ndim == 2 else a, g)
+                assert same.all(), (cfg, f, it.tile, int((~same).sum()))
+            n_checked += share
+    assert n_checked >= SAMPLE // 2
+    del runner
+    torch.cuda.empty_cache()
+
+
+def test_stage_in_and_trendline_stream_match_resident_path():
+    """bench.py's end-to-end pipeline (bands H2D from pinned memory into a two-slab ring, every
+    trendline plane D2H through TrendlineStream) writes what the device-resident step writes."""
+    fields = ['status', 'matched', 'class_val', 'onset_year', 'duration', 'magnitude'] + \
+        bench.TRENDLINE_FIELDS
+    c = bench.CONFIGS['c5']
+    m = Mosaic([3 * (1 << 20) + 4321], 1 << 20, 1, 0, 'by_scene')
+    eng = get_engine(0)
+    items = mosaic_inputs(m, c['years'], 1, 1, 0.0, 77, eng.device, bench.TARGET)
+    params, _ = compile_params(c['line_cost'], c['rules'], c['mode'])
+    fn = eng.compile_index(IndexProgram('B1 - B2', band_dtype='int16'))
+    runner = MosaicRunner(eng, m, params, items, fields, fn)
+    runner.step()
+    torch.cuda.synchronize()
+    ref = [{f: t.clone() for f, t in o.items()} for o in runner.outs]
+    for o in runner.outs:
+        for t in o.values():
+            t.fill_(0)
+    got = {}
+
+    def sink(f, row, host):
+        got.setdefault(f, []).append((row, host.clone()))
+
+    stage = bench._PinnedBands(items, eng.device)
+    d2h = TrendlineStream(m.tile * 8, eng.device, depth=4, sink=sink)
+    pushed = []
+
+    def after(k):
+        if k > 0:
+            d2h.push({f: runner.outs[k - 1][f] for f in bench.TRENDLINE_FIELDS},
+                     items[k - 1].tile.n)
+            pushed.append(k - 1)
+
+    runner.step(after_tile=after, stage_in=stage)
+    d2h.push({f: runner.outs[-1][f] for f in bench.TRENDLINE_FIELDS}, items[-1].tile.n)
+    pushed.append(len(items) - 1)
+    torch.cuda.synchronize()
+    d2h.drain()
+    for k, (o, r) in enumerate(zip(runner.outs, ref)):
+        n = items[k].tile.n
+        for f in fields:
+            assert torch.equal(o[f][..., :n], r[f][..., :n]), (k, f)
+    # the host copies: tile by tile, field by field, row by row, in push order
+    for f in bench.TRENDLINE_FIELDS:
+        rows = got[f]
+        Y = ref[0][f].shape[0]
+        assert len(rows) == Y * len(pushed)
+        for j, k in enumerate(pushed):
+            n = items[k].tile.n
+            for y in range(Y):
+                row, host = rows[j * Y + y]
+                assert row == y
+                want = ref[k][f][y, :n].cpu().contiguous().view(torch.uint8)
+                assert torch.equal(host, want), (f, k, y)

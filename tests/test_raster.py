@@ -28,11 +28,17 @@ def _tile(rows=12, cols=17, seed=3):
     return sc, meta, rules, out
 
 
+# numpy 1.x value-based promotion of `template_array * -99` (the reference pins numpy 1.7.1,
+# requirements.txt:7): -99 is an int8 scalar, so an unsigned template widens to the next signed type
+_LEGACY_TIMES_NODATA = {np.dtype(np.int16): np.int16, np.dtype(np.float32): np.float32,
+                        np.dtype(np.uint8): np.int16, np.dtype(np.uint16): np.int32,
+                        np.dtype(np.int8): np.int8, np.dtype(np.uint32): np.int64}
+
+
 def _data2raster_literal(points, shape, template_dtype):
     """utils.py:414-440 as written: holder = ones_like(template) * NODATA, holder[y, x] = float(v)
     (numpy's own assignment cast), then array2raster with data_type=compress=True: GDT_Byte."""
-    holder = np.ones(shape, template_dtype) * raster.NODATA
-    holder = holder.astype(template_dtype)
+    holder = np.ones(shape, _LEGACY_TIMES_NODATA[np.dtype(template_dtype)]) * raster.NODATA
     for (y, x), v in points:
         holder[y, x] = float(v)
     return raster.gdal_to_byte(holder)
@@ -41,7 +47,7 @@ def _data2raster_literal(points, shape, template_dtype):
 def test_label_rasters_reference_mode_matches_literal_data2raster():
     sc, meta, rules, out = _tile()
     rows, cols = 12, 17
-    for tdt in (np.int16, np.float32):
+    for tdt in (np.int16, np.float32, np.uint8, np.uint16):
         got = raster.label_rasters(out, rules, (rows, cols), template_dtype=tdt)
         for r, rule in enumerate(rules):
             for key in raster.LABEL_KEYS:
@@ -53,6 +59,20 @@ def test_label_rasters_reference_mode_matches_literal_data2raster():
                         pts.append(((p // cols, p % cols), v))
                 want = _data2raster_literal(pts, (rows, cols), tdt)
                 assert np.array_equal(got['%s_%s' % (rule.name, key)], want), (tdt, key)
+
+
+def test_holder_dtype_follows_numpy1_promotion():
+    for tdt, want in _LEGACY_TIMES_NODATA.items():
+        assert raster.holder_dtype(tdt) == np.dtype(want), tdt
+    # an unsigned template keeps NODATA at -99, which GDAL's Byte conversion writes as 0
+    out = raster.label_rasters({'matched': np.zeros((1, 4), np.uint8),
+                                'class_val': np.zeros((1, 4), np.int32),
+                                'onset_year': np.zeros((1, 4), np.int32),
+                                'duration': np.zeros((1, 4), np.int32),
+                                'magnitude': np.zeros((1, 4))},
+                               [LabelRule({'name': 'gd', 'val': 1, 'change_type': 'GD'})],
+                               (2, 2), template_dtype=np.uint16)
+    assert (out['gd_onset_year'] == 0).all()
 
 
 def test_label_rasters_typed_mode():
