@@ -10,7 +10,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, 'liblt_hip.so')
 
-LT_ABI_VERSION = 2
+LT_ABI_VERSION = 3
 LT_MAX_YEARS = 64
 LT_MAX_OBS = 1024
 LT_MAX_RULES = 16
@@ -73,6 +73,20 @@ class LtIndexProg(ctypes.Structure):
                 ('ops', LtIndexOp * LT_MAX_PROG)]
 
 
+class LtSettings(ctypes.Structure):
+    _fields_ = [('params', LtParams), ('target_year', ctypes.c_int32),
+                ('target_month', ctypes.c_int32), ('target_day', ctypes.c_int32),
+                ('n_index_bands', ctypes.c_int32), ('index_bands', ctypes.c_int32 * LT_MAX_BANDS),
+                ('index', LtIndexProg)]
+
+
+LT_EXC_NONE, LT_EXC_VALUE, LT_EXC_KEY, LT_EXC_TYPE, LT_EXC_ATTRIBUTE = 0, 1, 2, 3, 4
+LT_EXC_ZERO_DIVISION, LT_EXC_OTHER = 5, 6
+EXC_TYPES = {LT_EXC_VALUE: ValueError, LT_EXC_KEY: KeyError, LT_EXC_TYPE: TypeError,
+             LT_EXC_ATTRIBUTE: AttributeError, LT_EXC_ZERO_DIVISION: ZeroDivisionError,
+             LT_EXC_OTHER: Exception}
+
+
 class LtIndexIO(ctypes.Structure):
     _fields_ = [('n_pix', ctypes.c_int64), ('n_obs', ctypes.c_int64),
                 ('obs_stride', ctypes.c_int64), ('band_stride', ctypes.c_int64),
@@ -106,7 +120,8 @@ PIX_FIELDS = [('status', 'int32'), ('n_years', 'int32')]
 # symbols include/lt_abi.h declares (checked by tests/test_abi.py)
 EXPORTS = ['lt_abi_version', 'lt_ctx_create', 'lt_ctx_destroy', 'lt_last_error',
            'lt_analyze_tile', 'lt_analyze_tiles', 'lt_analyze_tiles_after', 'lt_label_tile', 'lt_ctx_set_timing', 'lt_ctx_stage_ms',
-           'lt_ctx_last_deferred', 'lt_index_codegen', 'lt_index_compile', 'lt_index_apply']
+           'lt_ctx_last_deferred', 'lt_index_codegen', 'lt_index_compile', 'lt_index_apply',
+           'lt_settings_compile']
 
 _LIB = None
 
@@ -146,6 +161,11 @@ def load_lib(path=None):
     lib.lt_index_codegen.restype = ctypes.c_int
     lib.lt_index_compile.argtypes = [vp, ctypes.POINTER(LtIndexProg), ctypes.POINTER(vp)]
     lib.lt_index_apply.argtypes = [vp, vp, ctypes.POINTER(LtIndexIO), vp]
+    lib.lt_settings_compile.argtypes = [ctypes.c_char_p, ctypes.c_int32, ctypes.c_int32,
+                                        ctypes.c_int32, ctypes.c_int32,
+                                        ctypes.POINTER(LtSettings),
+                                        ctypes.POINTER(ctypes.c_int32), ctypes.c_char_p,
+                                        ctypes.c_int64]
     if lib.lt_abi_version() != LT_ABI_VERSION:
         raise RuntimeError('liblt_hip.so ABI %d != %d' % (lib.lt_abi_version(), LT_ABI_VERSION))
     if path is None:

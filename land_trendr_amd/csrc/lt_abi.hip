@@ -15,31 +15,11 @@
 #include "lt_fast.h"
 #include "lt_pixel.h"
 #include "lt_index.h"
+#include "lt_settings.h"
 
 namespace {
 
 constexpr int kBlock = 256;
-
-// Stage 1: every pixel with the lazy DP. Pixels whose optimal path crosses an ambiguous column
-// are appended (wave-aggregated) to `defer` for the resolve stage.
-template <int MAXY>
-__global__ __launch_bounds__(kBlock) void analyze_kernel(const lt::DevScene* __restrict__ S,
-                                                         const lt_params P, const lt_tile_in in,
-                                                         const lt_tile_out out,
-                                                         int64_t* __restrict__ defer,
-                                                         unsigned long long* __restrict__ n_defer) {
-  const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (p >= in.n_pix) return;
-  const bool deferred = !lt::analyze_pixel<MAXY, true>(*S, P, in, out, p);
-  const uint64_t mask = __ballot(deferred);
-  if (mask == 0) return;
-  const int lane = threadIdx.x & 63;
-  const int leader = __ffsll((long long)mask) - 1;
-  unsigned long long base = 0;
-  if (lane == leader) base = atomicAdd(n_defer, (unsigned long long)__popcll(mask));
-  base = __shfl(base, leader);
-  if (deferred) defer[base + __popcll(mask & ((1ull << lane) - 1))] = p;
-}
 
 __device__ inline void defer_append(bool deferred, int64_t p, int lane, int64_t* __restrict__ list,
                                     unsigned long long* __restrict__ count) {
@@ -137,19 +117,6 @@ static unsigned resolve_grid(int device) {
   return cached;
 }
 
-// Stage 2 (per-lane reference body, lt_pixel.h): kept for the host harness's structure.
-template <int MAXY>
-__global__ __launch_bounds__(kBlock) void resolve_kernel(const lt::DevScene* __restrict__ S,
-                                                         const lt_params P, const lt_tile_in in,
-                                                         const lt_tile_out out,
-                                                         const int64_t* __restrict__ defer,
-                                                         const unsigned long long* __restrict__ n_defer) {
-  const int64_t n = (int64_t)*n_defer;
-  for (int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x; k < n;
-       k += (int64_t)gridDim.x * kBlock)
-    lt::analyze_pixel<MAXY, false>(*S, P, in, out, defer[k]);
-}
-
 struct YearArg {
   int32_t year[LT_MAX_YEARS];
 };
@@ -210,6 +177,28 @@ static int fail(lt_ctx* c, int code, const char* fmt, const char* detail = "") {
 extern "C" {
 
 int lt_abi_version(void) { return LT_ABI_VERSION; }
+
+int lt_settings_compile(const char* settings_json, int32_t pre_threshold_mode, int32_t band_type,
+                        int32_t out_type, int32_t raster_count, lt_settings* out,
+                        int32_t* exc_kind, char* err, int64_t err_cap) {
+  if (exc_kind) *exc_kind = LT_EXC_NONE;
+  if (err && err_cap > 0) err[0] = 0;
+  try {
+    lt_set::compile(settings_json, pre_threshold_mode, band_type, out_type, raster_count, out);
+    return LT_OK;
+  } catch (const lt_set::Fail& f) {
+    if (exc_kind) *exc_kind = f.exc;
+    if (err && err_cap > 0) {
+      const size_t n = f.msg.size() < (size_t)(err_cap - 1) ? f.msg.size() : (size_t)(err_cap - 1);
+      memcpy(err, f.msg.data(), n);
+      err[n] = 0;
+    }
+    return f.code;
+  } catch (...) {
+    if (exc_kind) *exc_kind = LT_EXC_OTHER;
+    return LT_ERR_ARG;
+  }
+}
 
 int lt_ctx_create(int device, lt_ctx** out) {
   if (!out) return LT_ERR_ARG;
@@ -444,6 +433,11 @@ int lt_analyze_tiles_after(lt_ctx* c, const lt_scene* sc, const lt_params* prm, 
     tmp.dist[k] = sc->dist[k];
   }
   if (!c->scene_valid || memcmp(&tmp, c->h_scene, sizeof tmp) != 0) {
+    // an earlier call, possibly on another stream, may still be reading d_scene: its last tile's
+    // resolve (side stream, in order, after every analyze it waited for) marks the end of all of
+    // that work, so the copy waits for it
+    if (c->set_used[0] || c->set_used[1])
+      HIP_OR_FAIL(c, hipStreamWaitEvent(stream, c->ev_resolved[c->last_set], 0));
     HIP_OR_FAIL(c, hipEventSynchronize(c->scene_copied));  // staging buffer free again
     memcpy(c->h_scene, &tmp, sizeof tmp);
     HIP_OR_FAIL(c, hipMemcpyAsync(c->d_scene, c->h_scene, sizeof tmp, hipMemcpyHostToDevice,

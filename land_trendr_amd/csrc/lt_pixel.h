@@ -158,8 +158,10 @@ struct RuleState {
 };
 
 // Screening bound: |LAPACK residual - closed-form residual| <= kScreen * sum(y^2) of the segment.
-// Measured worst case of the emulated dgelsd against the exact rational SSE is 2^-48 * sum(y^2)
-// (tests/test_screening.py), the closed form in double 2^-52: 2^-30 leaves a 2^18 margin.
+// tests/test_screening.py measures both against the exact rational SSE over ~1000 adversarial
+// segments (int16-range, non-integer, large-offset, nearly collinear, gapped x, m <= 64): the
+// emulated dgelsd stays within 2^-50 * sum(y^2), the kernel's closed form within 2^-49.5, their
+// difference within 2^-49.5 (the test requires 2^-40): 2^-30 leaves a margin of at least 2^10.
 constexpr double kScreen = 0x1p-30;
 
 // Observation value i of a tile: the f64 values, or the index raster in its stored type

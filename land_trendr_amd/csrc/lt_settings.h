@@ -1,0 +1,925 @@
+// lt_settings.h — lt_settings_compile: settings.json -> lt_params + target date + index program,
+// on the host, for callers that are not Python (include/lt_abi.h).
+//
+// Restates, with the same outcomes and exception kinds as the Python host (land_trendr_amd/
+// classes.py, settings.py, scene.py, index_eqn.py — tests/test_settings_abi.py checks the two
+// against each other on a corpus of settings and equations):
+//   * get_settings' json.load (utils.py:241) — a small JSON reader (NaN / Infinity accepted, as
+//     Python's json module accepts them);
+//   * LabelRule (classes.py:32-64) validation, and its compilation to lt_rule with the Python 2
+//     ordering of non-numeric qualifier values (classes._qual);
+//   * parse_date (utils.py:194-202): strptime('%Y-%m-%d') grammar;
+//   * index_eqn: parse_eqn_bands (utils.py:219-225) and the typed postfix program of
+//     index_eqn.IndexProgram (Python 2 / numpy 1.x semantics of rast_algebra's eval,
+//     utils.py:447-484): literal folding with Python 2 rules, numpy's legacy value-based
+//     promotion, constants placed where IndexProgram places them.
+#pragma once
+#include <ctype.h>
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "../../include/lt_abi.h"
+
+namespace lt_set {
+
+// ---- JSON ---------------------------------------------------------------------------------------
+struct JVal {
+  enum Kind { NUL, BOOL, INT, FLT, STR, ARR, OBJ } kind = NUL;
+  bool b = false;
+  __int128 i = 0;  // JSON integers of any size the corpus meets (Python ints are unbounded)
+  bool i_big = false;  // outside the __int128 range: kept as a float for comparisons only
+  double f = 0.0;
+  std::string s;
+  std::vector<JVal> a;
+  std::vector<std::pair<std::string, JVal>> o;  // insertion order; later duplicates win
+  const JVal* get(const char* key) const {
+    const JVal* r = nullptr;
+    for (auto& kv : o)
+      if (kv.first == key) r = &kv.second;
+    return r;
+  }
+  bool truthy() const {  // Python truth value of the json.load result
+    switch (kind) {
+      case NUL: return false;
+      case BOOL: return b;
+      case INT: return i_big || i != 0;
+      case FLT: return f != 0.0;  // NaN is truthy
+      case STR: return !s.empty();
+      case ARR: return !a.empty();
+      case OBJ: return !o.empty();
+    }
+    return false;
+  }
+  bool is_number() const { return kind == BOOL || kind == INT || kind == FLT; }
+  double as_double() const {
+    if (kind == BOOL) return b ? 1.0 : 0.0;
+    if (kind == FLT) return f;
+    return i_big ? f : (double)i;
+  }
+};
+
+struct JParser {
+  const char* p;
+  const char* end;
+  std::string err;
+  void ws() {
+    while (p < end && (*p == ' ' || *p == '\t' || *p == '\n' || *p == '\r')) p++;
+  }
+  bool lit(const char* w) {
+    size_t n = strlen(w);
+    if ((size_t)(end - p) >= n && memcmp(p, w, n) == 0) {
+      p += n;
+      return true;
+    }
+    return false;
+  }
+  static void utf8(std::string& out, uint32_t c) {
+    if (c < 0x80) out += (char)c;
+    else if (c < 0x800) { out += (char)(0xC0 | (c >> 6)); out += (char)(0x80 | (c & 0x3F)); }
+    else if (c < 0x10000) {
+      out += (char)(0xE0 | (c >> 12)); out += (char)(0x80 | ((c >> 6) & 0x3F));
+      out += (char)(0x80 | (c & 0x3F));
+    } else {
+      out += (char)(0xF0 | (c >> 18)); out += (char)(0x80 | ((c >> 12) & 0x3F));
+      out += (char)(0x80 | ((c >> 6) & 0x3F)); out += (char)(0x80 | (c & 0x3F));
+    }
+  }
+  bool hex4(uint32_t& v) {
+    if (end - p < 4) return false;
+    v = 0;
+    for (int k = 0; k < 4; k++) {
+      char c = *p++;
+      v <<= 4;
+      if (c >= '0' && c <= '9') v |= c - '0';
+      else if (c >= 'a' && c <= 'f') v |= c - 'a' + 10;
+      else if (c >= 'A' && c <= 'F') v |= c - 'A' + 10;
+      else return false;
+    }
+    return true;
+  }
+  bool str(std::string& out) {
+    if (p >= end || *p != '"') return false;
+    p++;
+    while (p < end && *p != '"') {
+      unsigned char c = (unsigned char)*p++;
+      if (c < 0x20) return false;
+      if (c != '\\') { out += (char)c; continue; }
+      if (p >= end) return false;
+      char e = *p++;
+      switch (e) {
+        case '"': out += '"'; break;
+        case '\\': out += '\\'; break;
+        case '/': out += '/'; break;
+        case 'b': out += '\b'; break;
+        case 'f': out += '\f'; break;
+        case 'n': out += '\n'; break;
+        case 'r': out += '\r'; break;
+        case 't': out += '\t'; break;
+        case 'u': {
+          uint32_t v;
+          if (!hex4(v)) return false;
+          if (v >= 0xD800 && v < 0xDC00 && end - p >= 6 && p[0] == '\\' && p[1] == 'u') {
+            const char* save = p;
+            p += 2;
+            uint32_t lo;
+            if (hex4(lo) && lo >= 0xDC00 && lo < 0xE000) v = 0x10000 + ((v - 0xD800) << 10) + (lo - 0xDC00);
+            else p = save;
+          }
+          utf8(out, v);
+          break;
+        }
+        default: return false;
+      }
+    }
+    if (p >= end) return false;
+    p++;
+    return true;
+  }
+  bool number(JVal& v) {
+    const char* s = p;
+    if (p < end && *p == '-') p++;
+    if (lit("Infinity")) { v.kind = JVal::FLT; v.f = *s == '-' ? -INFINITY : INFINITY; return true; }
+    if (p >= end || !(*p >= '0' && *p <= '9')) return false;
+    if (*p == '0') p++;
+    else while (p < end && *p >= '0' && *p <= '9') p++;
+    bool flt = false;
+    if (p < end && *p == '.') {
+      flt = true;
+      p++;
+      if (p >= end || !(*p >= '0' && *p <= '9')) return false;
+      while (p < end && *p >= '0' && *p <= '9') p++;
+    }
+    if (p < end && (*p == 'e' || *p == 'E')) {
+      flt = true;
+      p++;
+      if (p < end && (*p == '+' || *p == '-')) p++;
+      if (p >= end || !(*p >= '0' && *p <= '9')) return false;
+      while (p < end && *p >= '0' && *p <= '9') p++;
+    }
+    std::string t(s, p);
+    if (flt) {
+      v.kind = JVal::FLT;
+      v.f = strtod(t.c_str(), nullptr);
+      return true;
+    }
+    v.kind = JVal::INT;
+    __int128 acc = 0;
+    const bool neg = t[0] == '-';
+    for (size_t k = neg ? 1 : 0; k < t.size(); k++) {
+      if (acc > ((((__int128)1) << 120))) { v.i_big = true; break; }
+      acc = acc * 10 + (t[k] - '0');
+    }
+    v.i = neg ? -acc : acc;
+    if (v.i_big) v.f = strtod(t.c_str(), nullptr);
+    return true;
+  }
+  bool value(JVal& v, int depth = 0) {
+    if (depth > 64) return false;
+    ws();
+    if (p >= end) return false;
+    char c = *p;
+    if (c == '{') {
+      p++;
+      v.kind = JVal::OBJ;
+      ws();
+      if (p < end && *p == '}') { p++; return true; }
+      for (;;) {
+        ws();
+        std::string k;
+        if (!str(k)) return false;
+        ws();
+        if (p >= end || *p != ':') return false;
+        p++;
+        JVal x;
+        if (!value(x, depth + 1)) return false;
+        v.o.emplace_back(k, std::move(x));
+        ws();
+        if (p < end && *p == ',') { p++; continue; }
+        if (p < end && *p == '}') { p++; return true; }
+        return false;
+      }
+    }
+    if (c == '[') {
+      p++;
+      v.kind = JVal::ARR;
+      ws();
+      if (p < end && *p == ']') { p++; return true; }
+      for (;;) {
+        JVal x;
+        if (!value(x, depth + 1)) return false;
+        v.a.push_back(std::move(x));
+        ws();
+        if (p < end && *p == ',') { p++; continue; }
+        if (p < end && *p == ']') { p++; return true; }
+        return false;
+      }
+    }
+    if (c == '"') { v.kind = JVal::STR; return str(v.s); }
+    if (lit("null")) { v.kind = JVal::NUL; return true; }
+    if (lit("true")) { v.kind = JVal::BOOL; v.b = true; return true; }
+    if (lit("false")) { v.kind = JVal::BOOL; v.b = false; return true; }
+    if (lit("NaN")) { v.kind = JVal::FLT; v.f = NAN; return true; }
+    return number(v);
+  }
+};
+
+// Python str() of a json.load value, for error messages (Python 3 spelling)
+inline std::string py_str(const JVal& v, bool quote = false) {
+  char buf[64];
+  switch (v.kind) {
+    case JVal::NUL: return "None";
+    case JVal::BOOL: return v.b ? "True" : "False";
+    case JVal::INT:
+      if (v.i_big) { snprintf(buf, sizeof buf, "%.17g", v.f); return buf; }
+      snprintf(buf, sizeof buf, "%lld", (long long)v.i);
+      return buf;
+    case JVal::FLT:
+      if (isnan(v.f)) return "nan";
+      if (isinf(v.f)) return v.f > 0 ? "inf" : "-inf";
+      snprintf(buf, sizeof buf, "%.17g", v.f);
+      return buf;
+    case JVal::STR: return quote ? "'" + v.s + "'" : v.s;
+    case JVal::ARR: {
+      std::string r = "[";
+      for (size_t k = 0; k < v.a.size(); k++) r += (k ? ", " : "") + py_str(v.a[k], true);
+      return r + "]";
+    }
+    case JVal::OBJ: {
+      std::string r = "{";
+      for (size_t k = 0; k < v.o.size(); k++)
+        r += (k ? ", '" : "'") + v.o[k].first + "': " + py_str(v.o[k].second, true);
+      return r + "}";
+    }
+  }
+  return "";
+}
+
+struct Fail {
+  int code;
+  int exc;
+  std::string msg;
+};
+
+// ---- LabelRule (classes.py:32-64) + classes._qual ------------------------------------------------
+inline int qual_op(const JVal& q, const char* const* names, const int* ops, int n) {
+  if (q.kind != JVal::STR) return LT_Q_OTHER;
+  for (int k = 0; k < n; k++)
+    if (q.s == names[k]) return ops[k];
+  return LT_Q_OTHER;
+}
+
+inline void qual(const JVal* param, const char* const* names, const int* ops, int n, int32_t& op,
+                 double& val) {
+  op = LT_Q_UNSET;
+  val = 0.0;
+  if (!param || !param->truthy()) return;
+  op = qual_op(param->a[0], names, ops, n);
+  if (op == LT_Q_OTHER) return;
+  const JVal& v = param->a[1];
+  if (v.is_number()) {
+    val = v.as_double();
+    return;
+  }
+  // Python 2 ordering across types: a number is below any str/list/dict and above None
+  const bool num_lt_v = v.kind != JVal::NUL;
+  bool rejects = false;
+  switch (op) {
+    case LT_Q_EQ: rejects = true; break;
+    case LT_Q_LE: rejects = !num_lt_v; break;
+    case LT_Q_GE: rejects = num_lt_v; break;
+    case LT_Q_GT: rejects = num_lt_v; break;
+    case LT_Q_LT: rejects = !num_lt_v; break;
+  }
+  if (!rejects) {
+    op = LT_Q_OTHER;
+    return;
+  }
+  if (op == LT_Q_EQ || op == LT_Q_LE || op == LT_Q_GE) {
+    op = LT_Q_EQ;
+    val = NAN;
+  } else {
+    op = LT_Q_GT;
+    val = INFINITY;
+  }
+}
+
+// int(self.val) of classes.LabelRule.to_c, LT_NODATA where Python's int() raises
+inline int32_t class_val_of(const JVal& v) {
+  if (v.kind == JVal::BOOL) return v.b ? 1 : 0;
+  if (v.kind == JVal::INT) return v.i_big ? LT_NODATA : (int32_t)(int64_t)v.i;
+  if (v.kind == JVal::FLT) {
+    if (!isfinite(v.f)) return LT_NODATA;
+    return (int32_t)(int64_t)trunc(v.f);
+  }
+  if (v.kind == JVal::STR) {  // int('5'): optional blanks, sign, decimal digits (underscores ok)
+    const std::string& s = v.s;
+    size_t a = 0, b = s.size();
+    while (a < b && isspace((unsigned char)s[a])) a++;
+    while (b > a && isspace((unsigned char)s[b - 1])) b--;
+    bool neg = false;
+    if (a < b && (s[a] == '+' || s[a] == '-')) neg = s[a++] == '-';
+    if (a >= b) return LT_NODATA;
+    int64_t acc = 0;
+    bool prev_digit = false;
+    for (size_t k = a; k < b; k++) {
+      if (s[k] == '_' && prev_digit && k + 1 < b && isdigit((unsigned char)s[k + 1])) {
+        prev_digit = false;
+        continue;
+      }
+      if (!isdigit((unsigned char)s[k])) return LT_NODATA;
+      acc = acc * 10 + (s[k] - '0');
+      prev_digit = true;
+    }
+    return (int32_t)(neg ? -acc : acc);
+  }
+  return LT_NODATA;
+}
+
+inline void compile_rule(const JVal& opts, lt_rule& r) {
+  if (opts.kind != JVal::OBJ)  // options.get on a non-dict
+    throw Fail{LT_ERR_ARG, LT_EXC_ATTRIBUTE,
+               "'" + std::string(opts.kind == JVal::ARR ? "list" : opts.kind == JVal::STR ? "str"
+                                 : "object") + "' object has no attribute 'get'"};
+  const JVal* name = opts.get("name");
+  if (!name || !name->truthy()) throw Fail{LT_ERR_ARG, LT_EXC_VALUE, "name required"};
+  const JVal* val = opts.get("val");
+  if (!val || !val->truthy()) throw Fail{LT_ERR_ARG, LT_EXC_VALUE, "val required"};
+  const JVal* ct = opts.get("change_type");
+  int ctype = -1;
+  if (!ct || ct->kind == JVal::NUL) ctype = LT_CT_NONE;
+  else if (ct->kind == JVal::STR && ct->s == "FD") ctype = LT_CT_FD;
+  else if (ct->kind == JVal::STR && ct->s == "GD") ctype = LT_CT_GD;
+  else if (ct->kind == JVal::STR && ct->s == "LD") ctype = LT_CT_LD;
+  if (ctype < 0) throw Fail{LT_ERR_ARG, LT_EXC_VALUE, "Invalid change_type: " + py_str(*ct)};
+  const char* pnames[3] = {"onset_year", "duration", "pre_threshold"};
+  const JVal* params[3];
+  for (int k = 0; k < 3; k++) {
+    params[k] = opts.get(pnames[k]);
+    if (params[k] && params[k]->truthy() &&
+        (params[k]->kind != JVal::ARR || params[k]->a.size() != 2))
+      throw Fail{LT_ERR_ARG, LT_EXC_VALUE, std::string("Parameter ") + pnames[k] +
+                                               " - invalid value: " + py_str(*params[k])};
+  }
+  memset(&r, 0, sizeof r);
+  r.change_type = ctype;
+  static const char* const on_n[3] = {"=", "<=", ">="};
+  static const int on_o[3] = {LT_Q_EQ, LT_Q_LE, LT_Q_GE};
+  static const char* const cmp_n[2] = {">", "<"};
+  static const int cmp_o[2] = {LT_Q_GT, LT_Q_LT};
+  qual(params[0], on_n, on_o, 3, r.onset_op, r.onset_val);
+  qual(params[1], cmp_n, cmp_o, 2, r.duration_op, r.duration_val);
+  qual(params[2], cmp_n, cmp_o, 2, r.pre_op, r.pre_val);
+  r.class_val = class_val_of(*val);
+}
+
+// ---- parse_date (utils.py:194-202): strptime '%Y-%m-%d' -----------------------------------------
+inline bool parse_date(const std::string& s, int& y, int& m, int& d) {
+  // %Y: 4 digits; %m: 1[0-2]|0[1-9]|[1-9]; %d: 3[01]|[12]\d|0[1-9]|[1-9]| [1-9]; whole string
+  auto dig = [&](size_t k) { return k < s.size() && s[k] >= '0' && s[k] <= '9'; };
+  if (!(dig(0) && dig(1) && dig(2) && dig(3)) || s.size() < 5 || s[4] != '-') return false;
+  y = (s[0] - '0') * 1000 + (s[1] - '0') * 100 + (s[2] - '0') * 10 + (s[3] - '0');
+  size_t k = 5;
+  auto month2 = [&](size_t q) {
+    return q + 1 < s.size() && ((s[q] == '1' && s[q + 1] >= '0' && s[q + 1] <= '2') ||
+                                (s[q] == '0' && s[q + 1] >= '1' && s[q + 1] <= '9'));
+  };
+  if (month2(k) && k + 2 < s.size() && s[k + 2] == '-') {
+    m = (s[k] - '0') * 10 + (s[k + 1] - '0');
+    k += 3;
+  } else if (k < s.size() && s[k] >= '1' && s[k] <= '9' && k + 1 < s.size() && s[k + 1] == '-') {
+    m = s[k] - '0';
+    k += 2;
+  } else {
+    return false;
+  }
+  const size_t rest = s.size() - k;
+  if (rest == 2) {
+    const char a = s[k], b = s[k + 1];
+    if (a == '3' && (b == '0' || b == '1')) d = 30 + (b - '0');
+    else if ((a == '1' || a == '2') && b >= '0' && b <= '9') d = (a - '0') * 10 + (b - '0');
+    else if (a == '0' && b >= '1' && b <= '9') d = b - '0';
+    else if (a == ' ' && b >= '1' && b <= '9') d = b - '0';
+    else return false;
+  } else if (rest == 1 && s[k] >= '1' && s[k] <= '9') {
+    d = s[k] - '0';
+  } else {
+    return false;
+  }
+  static const int mdays[12] = {31, 28, 31, 30, 31, 30, 31, 31, 30, 31, 30, 31};
+  const bool leap = (y % 4 == 0 && y % 100 != 0) || y % 400 == 0;
+  const int dim = mdays[m - 1] + (m == 2 && leap ? 1 : 0);
+  return y >= 1 && d <= dim;
+}
+
+// ---- index_eqn (index_eqn.IndexProgram) ---------------------------------------------------------
+// numpy dtypes by (kind, size); F16 only arises as a scalar's min_scalar_type
+enum NT { I8, U8, I16, U16, I32, U32, I64, U64, F16, F32, F64, NT_BAD };
+inline char nt_kind(NT t) {
+  return (t == I8 || t == I16 || t == I32 || t == I64) ? 'i' : (t == F16 || t == F32 || t == F64) ? 'f' : 'u';
+}
+inline int nt_size(NT t) {
+  switch (t) {
+    case I8: case U8: return 1;
+    case I16: case U16: case F16: return 2;
+    case I32: case U32: case F32: return 4;
+    default: return 8;
+  }
+}
+inline NT nt_of_lt(int lt) {
+  switch (lt) {
+    case LT_T_F64: return F64; case LT_T_I16: return I16; case LT_T_U16: return U16;
+    case LT_T_I32: return I32; case LT_T_F32: return F32; case LT_T_U8: return U8;
+    case LT_T_U32: return U32; case LT_T_I8: return I8; case LT_T_I64: return I64;
+  }
+  return NT_BAD;
+}
+inline int lt_of_nt(NT t) {
+  switch (t) {
+    case F64: return LT_T_F64; case I16: return LT_T_I16; case U16: return LT_T_U16;
+    case I32: return LT_T_I32; case F32: return LT_T_F32; case U8: return LT_T_U8;
+    case U32: return LT_T_U32; case I8: return LT_T_I8; case I64: return LT_T_I64;
+    default: return -1;
+  }
+}
+inline NT int_of(char kind, int size) {
+  if (kind == 'i') return size == 1 ? I8 : size == 2 ? I16 : size == 4 ? I32 : I64;
+  return size == 1 ? U8 : size == 2 ? U16 : size == 4 ? U32 : U64;
+}
+// np.promote_types over these types
+inline NT promote(NT a, NT b) {
+  if (a == b) return a;
+  const char ka = nt_kind(a), kb = nt_kind(b);
+  const int sa = nt_size(a), sb = nt_size(b);
+  if (ka == 'f' && kb == 'f') return sa >= sb ? a : b;
+  if (ka == 'f' || kb == 'f') {
+    const NT f = ka == 'f' ? a : b, n = ka == 'f' ? b : a;
+    const int sn = nt_size(n);
+    NT need = sn == 1 ? F16 : sn == 2 ? F32 : F64;  // the float that holds every value of n
+    return nt_size(need) >= nt_size(f) ? need : f;
+  }
+  if (ka == kb) return sa >= sb ? a : b;
+  const NT s = ka == 'i' ? a : b, u = ka == 'i' ? b : a;
+  if (nt_size(u) < nt_size(s)) return s;
+  if (nt_size(u) == 8) return F64;
+  return int_of('i', 2 * nt_size(u));
+}
+
+struct Scalar {
+  bool is_float = false;
+  __int128 i = 0;
+  double f = 0.0;
+  double as_double() const { return is_float ? f : (double)i; }
+};
+
+// index_eqn._min_scalar_type
+inline NT min_scalar_type(const Scalar& v, bool signed_array) {
+  if (v.is_float) {
+    const double x = v.f;
+    if ((x > -65000 && x < 65000) || !isfinite(x)) return F16;
+    if (x > -3.4e38 && x < 3.4e38) return F32;
+    return F64;
+  }
+  static const NT sgn[4] = {I8, I16, I32, I64}, uns[4] = {U8, U16, U32, U64};
+  const NT* order = (v.i < 0 || signed_array) ? sgn : uns;
+  for (int k = 0; k < 4; k++) {
+    const int bits = 8 * nt_size(order[k]);
+    __int128 lo, hi;
+    if (nt_kind(order[k]) == 'i') {
+      lo = -(((__int128)1) << (bits - 1));
+      hi = (((__int128)1) << (bits - 1)) - 1;
+    } else {
+      lo = 0;
+      hi = (((__int128)1) << bits) - 1;
+    }
+    if (v.i >= lo && v.i <= hi) return order[k];
+  }
+  if (v.i >= 0 && signed_array && v.i <= ((((__int128)1) << 64) - 1)) return U64;
+  throw Fail{LT_ERR_ARG, LT_EXC_VALUE, "index_eqn: integer literal out of range"};
+}
+
+inline int kind_rank(char k) { return k == 'f' ? 2 : 1; }
+
+// index_eqn.result_dtype: a an array type, s a Python scalar
+inline NT result_scalar(NT t, const Scalar& s) {
+  const char sk = s.is_float ? 'f' : 'i';
+  if (kind_rank(sk) <= kind_rank(nt_kind(t))) return promote(t, min_scalar_type(s, nt_kind(t) == 'i'));
+  return promote(t, s.is_float ? F64 : I64);
+}
+
+struct Operand {
+  bool array = false;
+  NT t = NT_BAD;  // array type
+  Scalar s;       // scalar value
+};
+
+struct EqnCompiler {
+  std::string src;
+  size_t p = 0;
+  int depth = 0;  // parentheses (newlines allowed inside)
+  std::vector<int> bands;
+  NT band_t;
+  std::vector<lt_index_op> ops;
+
+  [[noreturn]] void syntax(const char* what) {
+    throw Fail{LT_ERR_ARG, LT_EXC_VALUE, std::string("index_eqn: invalid syntax (") + what + ")"};
+  }
+  void ws() {
+    for (;;) {
+      while (p < src.size() && (src[p] == ' ' || src[p] == '\t' || src[p] == '\f' ||
+                                ((src[p] == '\n' || src[p] == '\r') && depth > 0)))
+        p++;
+      if (p + 1 < src.size() && src[p] == '\\' && (src[p + 1] == '\n')) { p += 2; continue; }
+      break;
+    }
+  }
+  static bool idstart(char c) { return isalpha((unsigned char)c) || c == '_' || (unsigned char)c >= 0x80; }
+  static bool idchar(char c) { return isalnum((unsigned char)c) || c == '_' || (unsigned char)c >= 0x80; }
+
+  void push_const(const Scalar& s, size_t at) {
+    lt_index_op o;
+    memset(&o, 0, sizeof o);
+    if (s.is_float) {
+      o.op = LT_OP_CONST_F;
+      o.type = LT_T_F64;
+      o.fval = s.f;
+    } else {
+      o.op = LT_OP_CONST_I;
+      o.type = LT_T_I64;
+      o.ival = (int64_t)(uint64_t)s.i;  // ctypes c_int64 of a Python int: wraps mod 2^64
+    }
+    ops.insert(ops.begin() + at, o);
+  }
+  void push_op(int op, NT t) {
+    lt_index_op o;
+    memset(&o, 0, sizeof o);
+    o.op = op;
+    o.type = lt_of_nt(t);
+    if (o.type < 0) throw Fail{LT_ERR_ARG, LT_EXC_KEY, "index_eqn: unsupported result type"};
+    ops.push_back(o);
+  }
+
+  // a Python 3 numeric literal (the reference's Python 2 literals are a subset of what parses)
+  Scalar number() {
+    const size_t s0 = p;
+    Scalar r;
+    auto digits = [&](int base) {
+      bool any = false, prev_us = true;
+      while (p < src.size()) {
+        char c = src[p];
+        int dv = -1;
+        if (c >= '0' && c <= '9') dv = c - '0';
+        else if (c >= 'a' && c <= 'f') dv = c - 'a' + 10;
+        else if (c >= 'A' && c <= 'F') dv = c - 'A' + 10;
+        if (c == '_') {
+          if (prev_us && !(base != 10 && !any)) syntax("literal");
+          prev_us = true;
+          p++;
+          continue;
+        }
+        if (dv < 0 || dv >= base) break;
+        any = true;
+        prev_us = false;
+        p++;
+      }
+      if (prev_us && any) syntax("literal");
+      return any;
+    };
+    if (src[p] == '0' && p + 1 < src.size() && strchr("xXoObB", src[p + 1])) {
+      const char b = (char)tolower(src[p + 1]);
+      const int base = b == 'x' ? 16 : b == 'o' ? 8 : 2;
+      p += 2;
+      if (p < src.size() && src[p] == '_') p++;
+      const size_t d0 = p;
+      if (!digits(base)) syntax("literal");
+      __int128 acc = 0;
+      for (size_t k = d0; k < p; k++) {
+        if (src[k] == '_') continue;
+        const char c = (char)tolower(src[k]);
+        acc = acc * base + (c <= '9' ? c - '0' : c - 'a' + 10);
+        if (acc > ((((__int128)1) << 100))) syntax("literal too large");
+      }
+      r.i = acc;
+      if (p < src.size() && idchar(src[p])) syntax("literal");
+      return r;
+    }
+    bool flt = false;
+    if (src[p] != '.') digits(10);
+    if (p < src.size() && src[p] == '.') {
+      flt = true;
+      p++;
+      if (p < src.size() && src[p] >= '0' && src[p] <= '9') digits(10);
+    }
+    if (p < src.size() && (src[p] == 'e' || src[p] == 'E')) {
+      size_t q = p + 1;
+      if (q < src.size() && (src[q] == '+' || src[q] == '-')) q++;
+      if (q < src.size() && src[q] >= '0' && src[q] <= '9') {
+        flt = true;
+        p = q;
+        digits(10);
+      }
+    }
+    if (p < src.size() && (src[p] == 'j' || src[p] == 'J'))
+      throw Fail{LT_ERR_ARG, LT_EXC_VALUE, "index_eqn: unsupported expression (complex literal)"};
+    if (p < src.size() && idchar(src[p])) syntax("literal");
+    std::string t;
+    for (size_t k = s0; k < p; k++)
+      if (src[k] != '_') t += src[k];
+    if (flt) {
+      r.is_float = true;
+      r.f = strtod(t.c_str(), nullptr);
+      return r;
+    }
+    if (t.size() > 1 && t[0] == '0') {  // Python 3: no leading zeros on a non-zero decimal
+      for (char c : t)
+        if (c != '0') syntax("leading zeros");
+    }
+    __int128 acc = 0;
+    for (char c : t) {
+      acc = acc * 10 + (c - '0');
+      if (acc > ((((__int128)1) << 100))) syntax("literal too large");
+    }
+    r.i = acc;
+    return r;
+  }
+
+  static Scalar fold(int op, const Scalar& x, const Scalar& y) {
+    Scalar r;
+    if (!x.is_float && !y.is_float) {
+      switch (op) {
+        case LT_OP_ADD: r.i = x.i + y.i; break;
+        case LT_OP_SUB: r.i = x.i - y.i; break;
+        case LT_OP_MUL: r.i = x.i * y.i; break;
+        default: {  // Python 2 int / int and //: floor division
+          if (y.i == 0)
+            throw Fail{LT_ERR_ARG, LT_EXC_ZERO_DIVISION, "integer division or modulo by zero"};
+          __int128 q = x.i / y.i;
+          if ((x.i % y.i != 0) && ((x.i < 0) != (y.i < 0))) q -= 1;
+          r.i = q;
+        }
+      }
+      const __int128 lim = ((__int128)1) << 100;
+      if (r.i > lim || r.i < -lim) throw Fail{LT_ERR_ARG, LT_EXC_VALUE, "index_eqn: integer literal out of range"};
+      return r;
+    }
+    const double a = x.as_double(), b = y.as_double();
+    r.is_float = true;
+    switch (op) {
+      case LT_OP_ADD: r.f = a + b; break;
+      case LT_OP_SUB: r.f = a - b; break;
+      case LT_OP_MUL: r.f = a * b; break;
+      case LT_OP_DIV:
+        if (b == 0.0) throw Fail{LT_ERR_ARG, LT_EXC_ZERO_DIVISION, "float division by zero"};
+        r.f = a / b;
+        break;
+      default:
+        if (b == 0.0) throw Fail{LT_ERR_ARG, LT_EXC_ZERO_DIVISION, "float division by zero"};
+        r.f = floor(a / b);  // index_eqn._py2_binop: float(np.floor(x / y))
+    }
+    return r;
+  }
+
+  Operand atom() {
+    ws();
+    if (p >= src.size()) syntax("unexpected end");
+    const char c = src[p];
+    if (c == '(') {
+      p++;
+      depth++;
+      Operand o = expr();
+      ws();
+      if (p >= src.size() || src[p] != ')') syntax("')' expected");
+      p++;
+      depth--;
+      return o;
+    }
+    if ((c >= '0' && c <= '9') ||
+        (c == '.' && p + 1 < src.size() && src[p + 1] >= '0' && src[p + 1] <= '9')) {
+      Operand o;
+      o.s = number();
+      return o;
+    }
+    if (idstart(c)) {
+      const size_t s0 = p;
+      while (p < src.size() && idchar(src[p])) p++;
+      const std::string id = src.substr(s0, p - s0);
+      if (id.size() < 2 || id[0] != 'B')
+        throw Fail{LT_ERR_ARG, LT_EXC_VALUE, "index_eqn: unknown name '" + id + "'"};
+      for (size_t k = 1; k < id.size(); k++)
+        if (!(id[k] >= '0' && id[k] <= '9'))
+          throw Fail{LT_ERR_ARG, LT_EXC_VALUE, "index_eqn: unknown name '" + id + "'"};
+      const long num = strtol(id.c_str() + 1, nullptr, 10);
+      int slot = -1;
+      for (size_t k = 0; k < bands.size(); k++)
+        if (bands[k] == num) slot = (int)k;
+      lt_index_op o;
+      memset(&o, 0, sizeof o);
+      o.op = LT_OP_BAND;
+      o.type = lt_of_nt(band_t);
+      o.ival = slot;
+      ops.push_back(o);
+      Operand r;
+      r.array = true;
+      r.t = band_t;
+      return r;
+    }
+    syntax("unexpected character");
+  }
+
+  Operand unary() {
+    ws();
+    if (p < src.size() && (src[p] == '-' || src[p] == '+')) {
+      const bool neg = src[p] == '-';
+      p++;
+      Operand v = unary();
+      if (!v.array) {
+        if (neg) {
+          if (v.s.is_float) v.s.f = -v.s.f;
+          else v.s.i = -v.s.i;
+        }
+        return v;
+      }
+      if (neg) push_op(LT_OP_NEG, v.t);
+      return v;
+    }
+    Operand v = atom();
+    ws();
+    if (p + 1 < src.size() && src[p] == '*' && src[p + 1] == '*')
+      throw Fail{LT_ERR_ARG, LT_EXC_VALUE, "index_eqn: unsupported operator Pow"};
+    return v;
+  }
+
+  Operand binary(int op, Operand a, size_t n0, Operand b) {
+    if (!a.array && !b.array) {
+      Operand r;
+      r.s = fold(op, a.s, b.s);
+      return r;
+    }
+    NT t;
+    if (a.array && b.array) t = promote(a.t, b.t);
+    else t = result_scalar(a.array ? a.t : b.t, a.array ? b.s : a.s);
+    if (!a.array) push_const(a.s, n0);  // before the right operand's code
+    if (!b.array) push_const(b.s, ops.size());
+    push_op(op, t);
+    Operand r;
+    r.array = true;
+    r.t = t;
+    return r;
+  }
+
+  Operand term() {
+    size_t n0 = ops.size();
+    Operand a = unary();
+    for (;;) {
+      ws();
+      int op = 0;
+      if (p + 1 < src.size() && src[p] == '/' && src[p + 1] == '/') { op = LT_OP_FLOORDIV; p += 2; }
+      else if (p < src.size() && src[p] == '/') { op = LT_OP_DIV; p++; }
+      else if (p < src.size() && src[p] == '*' && !(p + 1 < src.size() && src[p + 1] == '*')) { op = LT_OP_MUL; p++; }
+      else if (p < src.size() && (src[p] == '%' || src[p] == '@'))
+        throw Fail{LT_ERR_ARG, LT_EXC_VALUE, "index_eqn: unsupported operator"};
+      else break;
+      Operand b = unary();
+      a = binary(op, a, n0, b);
+    }
+    return a;
+  }
+
+  Operand expr() {
+    size_t n0 = ops.size();
+    Operand a = term();
+    for (;;) {
+      ws();
+      int op = 0;
+      if (p < src.size() && src[p] == '+') op = LT_OP_ADD;
+      else if (p < src.size() && src[p] == '-') op = LT_OP_SUB;
+      else break;
+      p++;
+      Operand b = term();
+      a = binary(op, a, n0, b);
+    }
+    return a;
+  }
+};
+
+// index_eqn.parse_eqn_bands: every 'B<digits>' anywhere in the text, sorted, unique
+inline std::vector<int> eqn_bands(const std::string& e) {
+  std::vector<int> r;
+  for (size_t k = 0; k + 1 < e.size(); k++) {
+    if (e[k] != 'B' || !(e[k + 1] >= '0' && e[k + 1] <= '9')) continue;
+    size_t q = k + 1;
+    long long v = 0;
+    while (q < e.size() && e[q] >= '0' && e[q] <= '9') {
+      if (v < 100000000000LL) v = v * 10 + (e[q] - '0');
+      q++;
+    }
+    bool seen = false;
+    for (int b : r) seen = seen || b == v;
+    if (!seen) r.push_back((int)(v > 0x7fffffff ? 0x7fffffff : v));
+    k = q - 1;
+  }
+  std::sort(r.begin(), r.end());
+  return r;
+}
+
+inline void compile_index(const std::string& eqn, int band_type, int out_type, int raster_count,
+                          lt_settings* out) {
+  const NT bt = nt_of_lt(band_type);
+  const NT ot = nt_of_lt(out_type < 0 ? band_type : out_type);
+  if (bt == NT_BAD || ot == NT_BAD)
+    throw Fail{LT_ERR_ARG, LT_EXC_VALUE, "index_eqn: unsupported raster type"};
+  std::vector<int> bands = eqn_bands(eqn);
+  if (bands.empty())
+    throw Fail{LT_ERR_ARG, LT_EXC_VALUE, "index_eqn: '" + eqn + "' references no band"};
+  if (raster_count > 0 && bands.back() > raster_count)
+    throw Fail{LT_ERR_ARG, LT_EXC_OTHER,
+               "Band " + std::to_string(bands.back()) + " not present in <raster>"};
+  if (bands.front() <= 0)
+    throw Fail{LT_ERR_ARG, LT_EXC_OTHER, "Invalid band \"%s\" - bands must be >= 1"};
+  EqnCompiler c;
+  // eqn.strip(): Python's whitespace set
+  size_t a = 0, b = eqn.size();
+  while (a < b && isspace((unsigned char)eqn[a])) a++;
+  while (b > a && isspace((unsigned char)eqn[b - 1])) b--;
+  c.src = eqn.substr(a, b - a);
+  c.bands = bands;
+  c.band_t = bt;
+  Operand root = c.expr();
+  c.ws();
+  if (c.p != c.src.size()) c.syntax("trailing input");
+  NT rt;
+  if (!root.array) {  // a constant equation: numpy broadcasts it
+    c.push_const(root.s, c.ops.size());
+    rt = root.s.is_float ? F64 : I64;
+  } else {
+    rt = root.t;
+  }
+  (void)rt;
+  if ((int)c.ops.size() > LT_MAX_PROG)
+    throw Fail{LT_ERR_ARG, LT_EXC_VALUE,
+               "index_eqn: more than " + std::to_string(LT_MAX_PROG) + " operations"};
+  if ((int)bands.size() > LT_MAX_BANDS)
+    throw Fail{LT_ERR_ARG, LT_EXC_VALUE,
+               "index_eqn: more than " + std::to_string(LT_MAX_BANDS) + " bands"};
+  lt_index_prog& pr = out->index;
+  memset(&pr, 0, sizeof pr);
+  pr.n_ops = (int32_t)c.ops.size();
+  pr.n_bands = (int32_t)bands.size();
+  pr.band_type = lt_of_nt(bt);
+  pr.out_type = lt_of_nt(ot);
+  for (size_t k = 0; k < c.ops.size(); k++) pr.ops[k] = c.ops[k];
+  out->n_index_bands = (int32_t)bands.size();
+  for (size_t k = 0; k < bands.size(); k++) out->index_bands[k] = bands[k];
+}
+
+inline void compile(const char* json, int pre_mode, int band_type, int out_type, int raster_count,
+                    lt_settings* out) {
+  if (!json || !out) throw Fail{LT_ERR_ARG, LT_EXC_VALUE, "null argument"};
+  if (pre_mode != LT_PRE_REFERENCE && pre_mode != LT_PRE_DOCUMENTED)
+    throw Fail{LT_ERR_ARG, LT_EXC_VALUE,
+               "pre_threshold_mode must be \"reference\" or \"documented\""};
+  JParser jp{json, json + strlen(json), ""};
+  JVal root;
+  if (!jp.value(root)) throw Fail{LT_ERR_ARG, LT_EXC_VALUE, "settings: invalid JSON"};
+  jp.ws();
+  if (jp.p != jp.end) throw Fail{LT_ERR_ARG, LT_EXC_VALUE, "settings: invalid JSON (extra data)"};
+  if (root.kind != JVal::OBJ) throw Fail{LT_ERR_ARG, LT_EXC_TYPE, "settings: not a JSON object"};
+  memset(out, 0, sizeof *out);
+  // analysis_reducer: settings['line_cost'], settings['target_date'], settings['label_rules']
+  const JVal* lc = root.get("line_cost");
+  if (!lc) throw Fail{LT_ERR_ARG, LT_EXC_KEY, "'line_cost'"};
+  if (!lc->is_number())
+    throw Fail{LT_ERR_ARG, LT_EXC_TYPE, "line_cost must be a number"};
+  out->params.line_cost = lc->as_double();
+  out->params.pre_threshold_mode = pre_mode;
+  const JVal* td = root.get("target_date");
+  if (!td) throw Fail{LT_ERR_ARG, LT_EXC_KEY, "'target_date'"};
+  int y = 0, m = 0, d = 0;
+  if (td->kind != JVal::STR || !parse_date(td->s, y, m, d))
+    throw Fail{LT_ERR_ARG, LT_EXC_VALUE, "date_string must be in \"YYYY-MM-DD\" format"};
+  out->target_year = y;
+  out->target_month = m;
+  out->target_day = d;
+  const JVal* lr = root.get("label_rules");
+  if (lr) {
+    if (lr->kind != JVal::ARR) throw Fail{LT_ERR_ARG, LT_EXC_TYPE, "label_rules must be a list"};
+    if ((int)lr->a.size() > LT_MAX_RULES)
+      throw Fail{LT_ERR_LIMIT, LT_EXC_VALUE,
+                 "at most " + std::to_string(LT_MAX_RULES) + " label rules"};
+    for (size_t k = 0; k < lr->a.size(); k++) compile_rule(lr->a[k], out->params.rules[k]);
+    out->params.n_rules = (int32_t)lr->a.size();
+  }
+  const JVal* ie = root.get("index_eqn");
+  if (ie) {
+    if (ie->kind != JVal::STR) throw Fail{LT_ERR_ARG, LT_EXC_TYPE, "index_eqn must be a string"};
+    compile_index(ie->s, band_type, out_type, raster_count, out);
+  }
+}
+
+}  // namespace lt_set

@@ -77,6 +77,73 @@ def test_synthetic_c5_t40_low_cost_vs_oracle(engine):
                          'reference', n_years=40)
 
 
+@pytest.mark.parametrize('kind', ['eighths', 'offset1e6', 'offset2e7', 'f32_noise', 'f64'])
+def test_non_integer_and_large_offset_series_vs_oracle(engine, kind):
+    """Values the integer generator never makes, through every path of the analyze stage:
+    binary32-exact non-integers (k/8) and large offsets below 2^24 stay on the lazy binary32
+    path; offsets above 2^24 with odd values and arbitrary doubles take the binary64 resolve
+    (kDeferWide); small-variance noise on a large offset stresses the screening bound
+    (tests/test_screening.py). Every output field bit-exact against the oracle."""
+    import datetime as dt
+    from oracle import oracle
+    rng = np.random.default_rng(['eighths', 'offset1e6', 'offset2e7', 'f32_noise', 'f64'].index(
+        kind) + 300)
+    P, T = 4096, 30
+    dates = [dt.date(1985 + t, 6, 15) for t in range(T)]
+    base = np.round(rng.normal(0, 40, (T, P)))
+    trend = np.where(np.arange(T)[:, None] > rng.integers(3, 25, P)[None, :], -300.0, 0.0)
+    if kind == 'eighths':
+        vals = (1000 + base + trend) + rng.integers(0, 8, (T, P)) / 8.0
+    elif kind == 'offset1e6':
+        vals = 1e6 + base + trend
+    elif kind == 'offset2e7':
+        vals = 2e7 + 1 + 2 * (base + trend)
+    elif kind == 'f32_noise':
+        vals = (5e5 + rng.normal(0, 1e-2, (T, P)) + trend).astype(np.float32).astype(np.float64)
+    else:
+        vals = rng.uniform(-1, 1, (T, P)) + trend / 300.0
+    meta = build_scene(dates, parse_date('2014-07-01'))
+    for lc in (10.0, 0.5):
+        params, _ = compile_params(lc, [{'name': 'gd', 'val': 1, 'change_type': 'GD'},
+                                        {'name': 'fd', 'val': 2, 'change_type': 'FD'}])
+        got = _run(engine, meta, params, vals, None)
+        want = oracle.analyze_tile(meta, params, vals, None, n_threads=os.cpu_count() or 1)
+        for f in want:
+            a, b = want[f], got[f]
+            same = ((a.view(np.int64) == b.view(np.int64)) | (np.isnan(a) & np.isnan(b))
+                    if a.dtype.kind == 'f' else a == b)
+            assert same.all(), (kind, lc, f, int((~same).sum()))
+
+
+def test_two_scenes_on_two_streams_back_to_back(engine):
+    """The context keeps one device copy of the scene metadata: a call with a new scene on
+    another stream must not overwrite it while the previous call's kernels still read it."""
+    from land_trendr_amd.synth import make_scene
+    from oracle import oracle
+    dev = engine.device
+    scenes = []
+    for seed, years in ((31, 30), (32, 24)):
+        sc = make_scene(1 << 18, n_years=years, k_min=1, k_max=3, mask_prob=0.1, seed=seed)
+        meta = build_scene(sc.dates, parse_date('2014-07-01'))
+        scenes.append((sc, meta))
+    params, _ = compile_params(10, [{'name': 'gd', 'val': 1, 'change_type': 'GD'}])
+    streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+    ins = [(sc.values.to(dev), sc.valid.to(dev)) for sc, _ in scenes]
+    torch.cuda.synchronize()
+    outs = []
+    for (sc, meta), (v, m), st in zip(scenes, ins, streams):
+        outs.append(engine.analyze_tile(meta, params, v, m, stream=st))  # no sync in between
+    torch.cuda.synchronize()
+    for (sc, meta), out in zip(scenes, outs):
+        want = oracle.analyze_tile(meta, params, sc.values.numpy(), sc.valid.numpy(),
+                                   n_threads=os.cpu_count() or 1)
+        for f in ('status', 'matched', 'magnitude', 'val_fit', 'vertex', 'winner'):
+            a, b = want[f], out[f].cpu().numpy()
+            same = ((a.view(np.int64) == b.view(np.int64)) | (np.isnan(a) & np.isnan(b))
+                    if a.dtype.kind == 'f' else a == b)
+            assert same.all(), (meta.n_years, f, int((~same).sum()))
+
+
 def test_tie_heavy_small_integers_tiny_line_cost_vs_oracle(engine):
     """Small-integer series at line_cost 1e-4 (the reference tests' value) and 0.5: exact
     rational ties everywhere, singles/pairs on top of inexact OPT bases (provenance chains)."""
