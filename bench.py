@@ -16,6 +16,7 @@ D2H of the label rasters (and, for c5, of every per-year trendline plane) to the
 """
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -121,7 +122,10 @@ def cpu_baseline(cfg, seconds):
     """The oracle (C restatement, pthreads over every host core this process may use) on a
     bounded sample of the same configuration."""
     from oracle import oracle
-    threads, quota = host_cores()
+    avail, quota = host_cores()
+    # one thread per core the process may use: the cgroup quota when set (the GPU box shows the
+    # whole machine but grants a share; more threads than that only time-slice)
+    threads = avail if quota is None else max(1, min(avail, int(math.ceil(quota))))
     sample = max(64, 16 * threads)
     rate = None
     while True:
@@ -138,9 +142,8 @@ def cpu_baseline(cfg, seconds):
         if dt >= 0.5 * seconds or sample >= 4_000_000:
             break
         sample = int(min(4_000_000, max(sample * 2, rate * seconds)))
-    cores = threads if quota is None else min(threads, quota)
-    return {'value': rate / 1e6, 'unit': 'Mpixels/s', 'cores': round(cores, 2), 'kind': 'port',
-            'threads': threads, 'cgroup_cpu_quota': quota,
+    return {'value': rate / 1e6, 'unit': 'Mpixels/s', 'cores': threads, 'kind': 'port',
+            'threads': threads, 'host_cpus_visible': avail, 'cgroup_cpu_quota': quota,
             'sample': '%d synthetic px of the same config, oracle/lt_oracle.c, %d threads, %.1f s'
                       % (sample, threads, dt)}
 

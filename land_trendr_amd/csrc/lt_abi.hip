@@ -40,6 +40,11 @@ __device__ inline void defer_append(bool deferred, int64_t p, int lane, int64_t*
 #ifndef LT_FAST_WAVES_BIG
 #define LT_FAST_WAVES_BIG 4
 #endif
+// the analyze stage's phase probe: lt::NoProbe (nothing) except in the profiling build
+// (profiles/stamps.sh defines it as the cycle-stamping probe of profiles/stamp_probe.h)
+#ifndef LT_ANALYZE_PROBE
+#define LT_ANALYZE_PROBE lt::NoProbe
+#endif
 template <int MAXY, int RMAX>
 __global__ __launch_bounds__(64, (MAXY <= 32 && RMAX == 1) ? LT_FAST_WAVES_C2 : LT_FAST_WAVES_BIG) void analyze_fast_kernel(const lt::DevScene* __restrict__ S,
                                                           const lt_params P, const lt_tile_in in,
@@ -51,7 +56,8 @@ __global__ __launch_bounds__(64, (MAXY <= 32 && RMAX == 1) ? LT_FAST_WAVES_C2 : 
   const int lane = threadIdx.x;
   const int64_t p = (int64_t)blockIdx.x * 64 + lane;
   const bool live = p < in.n_pix;
-  const int d = lt::analyze_fast<MAXY, RMAX, false, float>(*S, P, in, out, xtab, p, live, lane, L);
+  const int d = lt::analyze_fast<MAXY, RMAX, false, float>(*S, P, in, out, xtab, p, live, lane, L,
+                                                           LT_ANALYZE_PROBE{});
   // two lists: [0, n_pix) for the binary32 resolve, [n_pix, 2 n_pix) for the binary64 one;
   // counters [0] / [2] count them (wave-aggregated atomics)
   defer_append(live && d == lt::kDeferExact, p, lane, defer, &n_defer[0]);

@@ -75,10 +75,20 @@ struct WaveLds {
 // EXACT = true (resolve stage): the exact-OPT DP, every column decided with the emulated LAPACK
 // residual of each start inside the error window; always kDone.
 enum { kDone = 0, kDeferExact = 1, kDeferWide = 2 };
-template <int MAXY, int RMAX, bool EXACT, class VT>
+
+// Phase probe of analyze_fast: probe.mark(k) is called by every lane at the end of phase k
+// (0 winner pick, 1 despike, 2 DP, 3 vertex fits + per-year walk + rule offers, 4 label writes).
+// The product kernels pass NoProbe, whose mark compiles to nothing; profiles/stamp_probe.h
+// defines the cycle-stamping probe of the profiling build (profiles/stamps.sh).
+struct NoProbe {
+  __device__ void mark(int) const {}
+};
+
+template <int MAXY, int RMAX, bool EXACT, class VT, class Probe = NoProbe>
 __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const lt_tile_in& in,
                                    const lt_tile_out& out, const lsq_xf* __restrict__ xtab,
-                                   int64_t p, bool live, int lane, WaveLds<MAXY, VT, EXACT>& L) {
+                                   int64_t p, bool live, int lane, WaveLds<MAXY, VT, EXACT>& L,
+                                   const Probe& probe = Probe()) {
   const int Y = S.n_years;
   const int64_t is = in.stride, os = out.stride;
   const double nan = __builtin_nan("");
@@ -167,6 +177,7 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
       }
     }
   }
+  probe.mark(0);
   // the reference raises for T < 2; non-binary32 values take the resolve stage's double path
   const bool ok = live && T >= 2 && !f32_bad;
   if (live && T == 0) status |= LT_ST_EMPTY;
@@ -264,6 +275,7 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
       }
     }
   }
+  probe.mark(1);
   const int nmax = wave_max(n);
 
   // ---- segmented least squares DP (utils.py:618-631), decided lazily ----
@@ -668,6 +680,7 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
       }
     }
   }
+  probe.mark(2);
   // deferred lanes stay in the wave (the loops below use wave collectives) but do nothing more
   if (deferred) vmask = 0;
 
@@ -777,12 +790,14 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
     pb = cb;
   }
 
+  probe.mark(3);
   // ---- change_labeling (utils.py:795-820) outputs ----
   if (live && !deferred) {
 #pragma unroll
     for (int r = 0; r < RMAX; r++)
       if (r < P.n_rules) rs[r].write(P.rules[r], out, (int64_t)r * os + p);
   }
+  probe.mark(4);
   if (!live || deferred) {
     if (!deferred) return kDone;
     if constexpr (EXACT) {  // a binary32 resolve given a value binary32 cannot hold: unreachable

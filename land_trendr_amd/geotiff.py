@@ -1,15 +1,18 @@
 """Minimal GeoTIFF reader for co-registered Landsat stacks (SURVEY.md §8(f)-2 ingest, first piece).
 
 The reference reads rasters with GDAL (`ds2array`, utils.py:272-282; `rast_algebra` :447-484);
-GDAL is not in this image. This reads the baseline TIFF subset such stacks use: little- or
-big-endian classic TIFF, strips or tiles, no compression (Compression = 1), chunky or planar
-bands, sample formats uint/int/float of 8/16/32/64 bits, plus the GeoTIFF/GDAL tags kept as raw
-values (ModelPixelScale, ModelTiepoint, GeoKeyDirectory, GDAL_NODATA). Returns numpy arrays in
-the file's sample type, [bands, rows, cols] — what `ds2array(ds, b)` gives per band.
+GDAL is not in this image. This reads the TIFF subset such stacks use: little- or big-endian
+classic TIFF, strips or tiles, uncompressed, LZW, Deflate or PackBits (tiffcodec.py; LZW
+native), horizontal / floating-point predictors, chunky or planar bands, sample formats
+uint/int/float of 8/16/32/64 bits, plus the GeoTIFF/GDAL tags kept as raw values
+(ModelPixelScale, ModelTiepoint, GeoKeyDirectory, GDAL_NODATA). Returns numpy arrays in the
+file's sample type, [bands, rows, cols] — what `ds2array(ds, b)` gives per band.
 """
 import struct
 
 import numpy as np
+
+from . import tiffcodec
 
 _TYPES = {1: ('B', 1), 2: ('s', 1), 3: ('H', 2), 4: ('I', 4), 5: ('II', 8), 6: ('b', 1),
           7: ('B', 1), 8: ('h', 2), 9: ('i', 4), 10: ('ii', 8), 11: ('f', 4), 12: ('d', 8),
@@ -47,8 +50,10 @@ class GeoTiff:
             raise TiffError('mixed bits per sample')
         self.bands = int(t.get(277, (1,))[0])
         fmt = int(t.get(339, (1,))[0])
-        if int(t.get(259, (1,))[0]) != 1:
-            raise TiffError('compressed TIFF (Compression=%d) is not supported' % t[259][0])
+        self.compression = int(t.get(259, (1,))[0])
+        if self.compression not in (1, 5, 8, 32946, 32773):
+            raise TiffError('TIFF compression %d is not supported' % self.compression)
+        self.predictor = int(t.get(317, (1,))[0])
         if (fmt, self.bits) not in _SAMPLE:
             raise TiffError('sample format %d / %d bits not supported' % (fmt, self.bits))
         self.dtype = np.dtype(_SAMPLE[(fmt, self.bits)]).newbyteorder(self._bo)
@@ -104,36 +109,58 @@ class GeoTiff:
                 tags[tag] = struct.unpack(bo + code * cnt, raw)
         return tags
 
+    def _chunk(self, k, rows, cols, spp):
+        """Decoded samples of strip / tile k: [rows, cols * spp] in the file's byte order."""
+        t, d = self.tags, self._d
+        offs = t[273] if 273 in t else t[324]
+        counts = t[279] if 279 in t else t[325]
+        size = rows * cols * spp * self.dtype.itemsize
+        try:
+            raw = tiffcodec.decode(self.compression, d[offs[k]:offs[k] + counts[k]], size)
+        except ValueError as e:
+            raise TiffError(str(e))
+        block = np.frombuffer(raw.tobytes(), self.dtype, rows * cols * spp).reshape(
+            rows, cols * spp)
+        try:
+            return tiffcodec.undo_predictor(block, self.predictor, self.dtype, cols, spp)
+        except ValueError as e:
+            raise TiffError(str(e))
+
     def read(self):
         """All bands as a [bands, rows, cols] array in the sample type (native byte order)."""
-        t, d = self.tags, self._d
-        item = self.dtype.itemsize
+        t = self.tags
+        W, H, B = self.width, self.height, self.bands
+        spp = B if self.planar == 1 else 1
         if 273 in t:  # strips
-            offs, counts = t[273], t[279]
-            raw = b''.join(d[o:o + c] for o, c in zip(offs, counts))
-            if self.planar == 1:
-                a = np.frombuffer(raw, self.dtype, self.width * self.height * self.bands)
-                a = a.reshape(self.height, self.width, self.bands).transpose(2, 0, 1)
-            else:
-                a = np.frombuffer(raw, self.dtype, self.width * self.height * self.bands)
-                a = a.reshape(self.bands, self.height, self.width)
+            rps = min(int(t.get(278, (H,))[0]), H)
+            per_band = -(-H // rps)
+            a = np.empty((B, H, W), self.dtype)
+            for k in range(len(t[273])):
+                b0, r = (0, k) if self.planar == 1 else (k // per_band, k % per_band)
+                y0 = r * rps
+                rows = min(rps, H - y0)
+                if rows <= 0 or b0 >= B:
+                    continue
+                blk = self._chunk(k, rows, W, spp)
+                if self.planar == 1:
+                    a[:, y0:y0 + rows, :] = blk.reshape(rows, W, B).transpose(2, 0, 1)
+                else:
+                    a[b0, y0:y0 + rows, :] = blk
         elif 324 in t:  # tiles
             tw, th = int(t[322][0]), int(t[323][0])
-            offs = t[324]
-            tx, ty = -(-self.width // tw), -(-self.height // th)
+            tx, ty = -(-W // tw), -(-H // th)
             per_band = tx * ty
-            a = np.empty((self.bands, ty * th, tx * tw), self.dtype)
-            for k, o in enumerate(offs):
-                spp = self.bands if self.planar == 1 else 1
-                tile = np.frombuffer(d[o:o + tw * th * spp * item], self.dtype, tw * th * spp)
+            a = np.empty((B, ty * th, tx * tw), self.dtype)
+            for k in range(len(t[324])):
                 b0 = 0 if self.planar == 1 else k // per_band
                 r = k % per_band
                 yy, xx = (r // tx) * th, (r % tx) * tw
+                blk = self._chunk(k, th, tw, spp)
                 if self.planar == 1:
-                    a[:, yy:yy + th, xx:xx + tw] = tile.reshape(th, tw, spp).transpose(2, 0, 1)
+                    a[:, yy:yy + th, xx:xx + tw] = blk.reshape(th, tw, spp).transpose(2, 0, 1)
                 else:
-                    a[b0, yy:yy + th, xx:xx + tw] = tile.reshape(th, tw)
-            a = a[:, :self.height, :self.width]
+                    a[b0, yy:yy + th, xx:xx + tw] = blk
+            a = a[:, :H, :W]
         else:
             raise TiffError('no strip or tile offsets')
         return np.ascontiguousarray(a).astype(self.dtype.newbyteorder('='), copy=False)

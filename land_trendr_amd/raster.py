@@ -17,8 +17,8 @@ GDT_Byte. GDAL then saturates every value into 0..255 (-99
 
 Keys follow the reference: '<rule>_<field>' for labels (mr_land_trendr_job.py:120-126) and
 'trendline/<YYYY-MM-DD>-<attr>' per winning acquisition date for the trendline planes
-(classes.py:100-116). Files are written by write_geotiff: uncompressed GeoTIFF with the template's
-georeferencing tags copied (the reference asks GDAL for LZW: a storage detail, values equal).
+(classes.py:100-116). Files are written by write_geotiff: LZW-compressed GeoTIFF (the reference's
+COMPRESS=LZW, utils.py:386) with the template's georeferencing tags copied.
 """
 import struct
 
@@ -135,20 +135,35 @@ _SAMPLE_FORMAT = {'u': 1, 'i': 2, 'f': 3}
 _GEO_TAGS = (33550, 33922, 34264, 34735, 34736, 34737)  # scale, tiepoint, transform, geokeys ...
 
 
-def write_geotiff(path, array, template=None, nodata=NODATA, geotransform=None):
-    """Uncompressed little-endian GeoTIFF of a 2-D array, or of a 3-D [bands, rows, cols] array
-    (planar configuration 2: one strip per band, what GeoTiff.read returns as [bands, rows, cols]);
-    georeferencing tags copied verbatim from `template` (a GeoTiff or a path), or written from a
-    north-up `geotransform` (ModelPixelScale + ModelTiepoint), GDAL_NODATA set to `nodata`."""
+def write_geotiff(path, array, template=None, nodata=NODATA, geotransform=None, compress='lzw',
+                  predictor=1, rows_per_strip=None):
+    """Little-endian GeoTIFF of a 2-D array, or of a 3-D [bands, rows, cols] array (planar
+    configuration 2: each band's strips in turn, what GeoTiff.read returns as [bands, rows,
+    cols]); georeferencing tags copied verbatim from `template` (a GeoTiff or a path), or written
+    from a north-up `geotransform` (ModelPixelScale + ModelTiepoint), GDAL_NODATA set to `nodata`.
+    compress: 'lzw' (array2raster's COMPRESS=LZW, utils.py:386; the native codec of
+    tiffcodec.py), 'deflate' or None; predictor 2 (horizontal differencing) for integer samples.
+    Strips of about 8 KB of raw samples, as GDAL's GTiff driver lays them out."""
+    from . import tiffcodec
     a = np.ascontiguousarray(array)
     if a.ndim not in (2, 3) or a.dtype.kind not in _SAMPLE_FORMAT:
         raise ValueError('write_geotiff: 2-D or 3-D integer or float array required')
+    comp = {None: 1, 'none': 1, 'lzw': 5, 'deflate': 8}[compress]
+    if predictor not in (1, 2) or (predictor == 2 and a.dtype.kind == 'f'):
+        raise ValueError('write_geotiff: predictor 1, or 2 for integer samples')
     a = a.astype(a.dtype.newbyteorder('<'), copy=False)
     if a.ndim == 2:
         a = a[None]
     nb, rows, cols = a.shape
     tmpl = GeoTiff(template) if isinstance(template, str) else template
-    plane = rows * cols * a.dtype.itemsize
+    rps = rows_per_strip or max(1, min(rows, 8192 // max(1, cols * a.dtype.itemsize)))
+    strips = []
+    for b in range(nb):
+        for y0 in range(0, rows, rps):
+            blk = a[b, y0:y0 + rps]
+            if predictor == 2:
+                blk = tiffcodec.apply_predictor2(blk, cols, 1)
+            strips.append(tiffcodec.encode(comp, np.ascontiguousarray(blk).tobytes()))
 
     def layout(data_off):
         entries = []  # (tag, type, count, payload bytes)
@@ -157,16 +172,22 @@ def write_geotiff(path, array, template=None, nodata=NODATA, geotransform=None):
             payload = struct.pack('<' + fmt * len(values), *values)
             entries.append((tag, typ, len(values), payload))
 
+        offs, o = [], data_off
+        for st in strips:
+            offs.append(o)
+            o += len(st)
         add(256, 4, [cols], 'I')
         add(257, 4, [rows], 'I')
         add(258, 3, [a.dtype.itemsize * 8] * nb, 'H')
-        add(259, 3, [1], 'H')
+        add(259, 3, [comp], 'H')
         add(262, 3, [1], 'H')
-        add(273, 4, [data_off + b * plane for b in range(nb)], 'I')
+        add(273, 4, offs, 'I')
         add(277, 3, [nb], 'H')
-        add(278, 4, [rows], 'I')
-        add(279, 4, [plane] * nb, 'I')
+        add(278, 4, [rps], 'I')
+        add(279, 4, [len(st) for st in strips], 'I')
         add(284, 3, [2 if nb > 1 else 1], 'H')
+        if predictor == 2:
+            add(317, 3, [2], 'H')
         add(339, 3, [_SAMPLE_FORMAT[a.dtype.kind]] * nb, 'H')
         if tmpl is not None:
             for tag in _GEO_TAGS:
@@ -210,16 +231,19 @@ def write_geotiff(path, array, template=None, nodata=NODATA, geotransform=None):
     data_off = layout(0)[3]
     ifd_off, ifd, extra, end = layout(data_off)
     assert end == data_off
+    if data_off + sum(len(st) for st in strips) >= 1 << 32:
+        raise ValueError('write_geotiff: over 4 GiB needs BigTIFF, which is not written')
     with open(path, 'wb') as f:
         f.write(b'II*\x00' + struct.pack('<I', ifd_off))
         f.write(ifd)
         f.write(extra)
         f.write(b'\x00' * (data_off - ifd_off - len(ifd) - len(extra)))
-        f.write(a.tobytes())
+        for st in strips:
+            f.write(st)
     return path
 
 
-def output_reducer(rasters, template, out_dir, job='job'):
+def output_reducer(rasters, template, out_dir, job='job', compress='lzw'):
     """The file side of output_reducer (mr_land_trendr_job.py:128-152) without S3: every key's
     raster written as <out_dir>/<job>/output/rasters/<key>.tif (settings.py OUT_RAST_KEYNAME) with
     the template's georeferencing. Yields (key, [path]) like the reducer yields (key, [s3 key])."""
@@ -228,5 +252,5 @@ def output_reducer(rasters, template, out_dir, job='job'):
     for key in sorted(rasters):
         path = os.path.join(out_dir, '%s/output/rasters/%s.tif' % (job, key))
         os.makedirs(os.path.dirname(path), exist_ok=True)
-        write_geotiff(path, rasters[key], template=tmpl)
+        write_geotiff(path, rasters[key], template=tmpl, compress=compress)
         yield key, [path]

@@ -1,0 +1,123 @@
+"""TIFF strip / tile codecs for the GeoTIFF reader and writer (what GDAL does for the reference:
+ds2array decodes any compression, utils.py:272-282; array2raster writes COMPRESS=LZW, :386).
+
+  * LZW (Compression 5): native, land_trendr_amd/liblt_io.so (include/lt_io.h);
+  * Deflate (Compression 8 and the old 32946): zlib;
+  * PackBits (Compression 32773): restated here (run-length, byte oriented);
+  * Predictor 2 (horizontal differencing, integer samples) undone / applied per row;
+    Predictor 3 (floating point) is decoded too (byte planes, then differencing).
+"""
+import ctypes
+import os
+import zlib
+
+import numpy as np
+
+_LIB = None
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'liblt_io.so')
+
+
+def _lib():
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError('%s not built: run __graft_entry__.build()' % LIB_PATH)
+        L = ctypes.CDLL(LIB_PATH)
+        for f in (L.lt_lzw_decode, L.lt_lzw_encode):
+            f.argtypes = [ctypes.c_char_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64]
+            f.restype = ctypes.c_int64
+        _LIB = L
+    return _LIB
+
+
+def lzw_decode(data, size):
+    """One LZW strip -> `size` raw bytes (a short strip is zero-padded, as libtiff does)."""
+    out = np.zeros(size, np.uint8)
+    n = _lib().lt_lzw_decode(bytes(data), len(data), out.ctypes.data, size)
+    if n < 0:
+        raise ValueError('LZW: corrupt strip (%d)' % n)
+    return out
+
+
+def lzw_encode(raw):
+    raw = bytes(raw)
+    cap = len(raw) * 3 // 2 + 16
+    out = np.empty(cap, np.uint8)
+    n = _lib().lt_lzw_encode(raw, len(raw), out.ctypes.data, cap)
+    if n < 0:
+        raise ValueError('LZW: encode failed (%d)' % n)
+    return out[:n].tobytes()
+
+
+def packbits_decode(data, size):
+    out = bytearray()
+    i, d = 0, bytes(data)
+    while i < len(d) and len(out) < size:
+        n = d[i] - 256 if d[i] > 127 else d[i]
+        i += 1
+        if n >= 0:
+            out += d[i:i + n + 1]
+            i += n + 1
+        elif n != -128:
+            out += d[i:i + 1] * (1 - n)
+            i += 1
+    out = out[:size]
+    return np.frombuffer(bytes(out) + b'\x00' * (size - len(out)), np.uint8)
+
+
+def decode(compression, data, size):
+    """Raw bytes of one strip or tile."""
+    if compression == 1:
+        b = np.frombuffer(bytes(data[:size]), np.uint8)
+        return b if len(b) == size else np.concatenate([b, np.zeros(size - len(b), np.uint8)])
+    if compression == 5:
+        return lzw_decode(data, size)
+    if compression in (8, 32946):
+        raw = zlib.decompress(bytes(data))
+        b = np.frombuffer(raw[:size], np.uint8)
+        return b if len(b) == size else np.concatenate([b, np.zeros(size - len(b), np.uint8)])
+    if compression == 32773:
+        return packbits_decode(data, size)
+    raise ValueError('TIFF compression %d is not supported' % compression)
+
+
+def encode(compression, raw):
+    if compression == 1:
+        return bytes(raw)
+    if compression == 5:
+        return lzw_encode(raw)
+    if compression == 8:
+        return zlib.compress(bytes(raw), 6)
+    raise ValueError('TIFF compression %d is not supported for writing' % compression)
+
+
+def undo_predictor(block, predictor, dtype, width, spp):
+    """block: [rows, width * spp] samples of one strip / tile (file byte order) -> undone."""
+    if predictor == 1:
+        return block
+    if predictor == 2:
+        rows = block.shape[0]
+        a = block.reshape(rows, width, spp)
+        # cumulative sum along each row in the sample type: integer wrap, as libtiff's
+        # horizontal accumulation does
+        u = a.astype(a.dtype.newbyteorder('='))
+        acc = np.cumsum(u, axis=1, dtype=u.dtype)
+        return acc.astype(a.dtype).reshape(rows, width * spp)
+    if predictor == 3:  # floating point: bytes split into planes (MSB first), then differenced
+        rows = block.shape[0]
+        item = dtype.itemsize
+        raw = block.view(np.uint8).reshape(rows, width * spp * item)
+        raw = np.cumsum(raw, axis=1, dtype=np.uint8)
+        planes = raw.reshape(rows, item, width * spp)
+        be = planes.transpose(0, 2, 1)  # [rows, samples, bytes MSB first]
+        out = np.ascontiguousarray(be).view(dtype.newbyteorder('>')).reshape(rows, width * spp)
+        return out.astype(dtype)
+    raise ValueError('TIFF predictor %d is not supported' % predictor)
+
+
+def apply_predictor2(block, width, spp):
+    rows = block.shape[0]
+    a = block.reshape(rows, width, spp)
+    d = a.copy()
+    d[:, 1:] = a[:, 1:] - a[:, :-1]  # wraps in the integer type
+    return d.reshape(rows, width * spp)

@@ -1,0 +1,113 @@
+"""Compressed GeoTIFF IO: the native LZW codec (liblt_io.so, include/lt_io.h)
+and the reader / writer around it, checked against libtiff — the library GDAL itself uses for TIFF
+compression — through Pillow's libtiff plugin when it is importable (CPU-only tests)."""
+import io
+import os
+
+import numpy as np
+import pytest
+
+from land_trendr_amd import raster, tiffcodec
+from land_trendr_amd.geotiff import GeoTiff
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TIF = os.path.join(ROOT, 'tests', 'golden', 'files', 'dummy_single_band.tif')
+
+try:
+    from PIL import Image, features
+    HAVE_LIBTIFF = features.check('libtiff')
+except ImportError:  # pragma: no cover
+    HAVE_LIBTIFF = False
+needs_libtiff = pytest.mark.skipif(not HAVE_LIBTIFF, reason='Pillow with libtiff not importable')
+
+
+@pytest.mark.parametrize('kind', ['empty', 'one', 'zeros', 'ramp', 'random', 'lowentropy', 'big'])
+def test_lzw_round_trip(kind):
+    rng = np.random.default_rng(len(kind))
+    data = {'empty': b'', 'one': b'\x07', 'zeros': bytes(100000),
+            'ramp': bytes(range(256)) * 300,
+            'random': rng.integers(0, 256, 70000, dtype=np.uint8).tobytes(),
+            'lowentropy': rng.integers(0, 3, 300000, dtype=np.uint8).tobytes(),
+            'big': (np.arange(2_000_000) % 251).astype(np.uint8).tobytes()}[kind]
+    enc = tiffcodec.lzw_encode(data)
+    assert tiffcodec.lzw_decode(enc, len(data)).tobytes() == data
+    if kind in ('zeros', 'lowentropy'):
+        assert len(enc) < len(data) // 4
+
+
+def test_lzw_decodes_the_tiff_spec_stream_shape():
+    """A hand-built code stream: Clear, 'A' 'B', the new code 258 ('AB'), EOI (9-bit codes, MSB
+    first), decodes to 'ABAB'."""
+    codes = [256, 65, 66, 258, 257]
+    bits = ''.join(format(c, '09b') for c in codes)
+    bits += '0' * (-len(bits) % 8)
+    stream = bytes(int(bits[i:i + 8], 2) for i in range(0, len(bits), 8))
+    assert tiffcodec.lzw_decode(stream, 4).tobytes() == b'ABAB'
+
+
+def _pil_write(path, a, compression):
+    Image.fromarray(a).save(path, compression=compression)
+
+
+def _pil_read(path):
+    return np.array(Image.open(path))
+
+
+@needs_libtiff
+@pytest.mark.parametrize('dtype', [np.uint8, np.uint16, np.float32, np.int32])
+@pytest.mark.parametrize('compression', ['tiff_lzw', 'tiff_adobe_deflate', 'packbits'])
+def test_reader_decodes_libtiff_output(tmp_path, dtype, compression):
+    rng = np.random.default_rng(7)
+    a = (rng.normal(300, 90, (123, 457))).astype(dtype) if dtype != np.float32 else \
+        rng.normal(0, 1, (123, 457)).astype(np.float32)
+    a[:, :40] = a[0, 0]  # some runs
+    p = str(tmp_path / 'x.tif')
+    _pil_write(p, a, compression)
+    g = GeoTiff(p)
+    assert g.compression in (5, 8, 32946, 32773)
+    got = g.read()[0]
+    assert got.dtype == a.dtype and np.array_equal(got, a)
+
+
+@needs_libtiff
+@pytest.mark.parametrize('dtype', [np.uint8, np.uint16, np.float32, np.int32])
+@pytest.mark.parametrize('compress,predictor', [('lzw', 1), ('deflate', 1), ('lzw', 2)])
+def test_writer_output_decodes_in_libtiff(tmp_path, dtype, compress, predictor):
+    if predictor == 2 and dtype == np.float32:
+        pytest.skip('horizontal predictor is for integer samples')
+    rng = np.random.default_rng(11)
+    a = rng.integers(0, 200, (301, 77)).astype(dtype)
+    a[100:150] = 5
+    p = str(tmp_path / 'y.tif')
+    raster.write_geotiff(p, a, template=TIF, compress=compress, predictor=predictor)
+    assert np.array_equal(_pil_read(p), a)
+    g = GeoTiff(p)
+    assert np.array_equal(g.read()[0], a) and g.compression == (5 if compress == 'lzw' else 8)
+
+
+def test_writer_round_trip_all_types_and_bands(tmp_path):
+    tmpl = GeoTiff(TIF)
+    for dt in (np.uint8, np.int8, np.int16, np.uint16, np.int32, np.float32, np.float64):
+        a = (np.arange(3 * 45 * 54).reshape(3, 45, 54) % 117 - 40).astype(dt)
+        for compress in ('lzw', 'deflate', None):
+            f = str(tmp_path / ('o_%s_%s.tif' % (np.dtype(dt).name, compress)))
+            raster.write_geotiff(f, a, template=tmpl, compress=compress)
+            g = GeoTiff(f)
+            assert np.array_equal(g.read(), a) and g.read().dtype == dt
+            assert g.pixel_scale == tmpl.pixel_scale and g.geokeys == tmpl.geokeys
+
+
+def test_lzw_scene_sized_raster_is_fast_enough(tmp_path):
+    """A 7000 x 7000 GDT_Byte label raster (what output_reducer writes per key) in seconds."""
+    import time
+    rng = np.random.default_rng(3)
+    a = np.where(rng.random((7000, 7000)) < 0.3, rng.integers(0, 255, (7000, 7000)), 0).astype(
+        np.uint8)
+    p = str(tmp_path / 'big.tif')
+    t0 = time.perf_counter()
+    raster.write_geotiff(p, a, compress='lzw')
+    t1 = time.perf_counter()
+    got = GeoTiff(p).read()[0]
+    t2 = time.perf_counter()
+    assert np.array_equal(got, a)
+    assert t1 - t0 < 30 and t2 - t1 < 30, (t1 - t0, t2 - t1)
