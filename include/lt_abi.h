@@ -191,6 +191,31 @@ typedef struct {
   const uint8_t* present;     /* [Y][stride] device, 0 = no point in this slot; NULL = all  */
 } lt_label_in;
 
+/* ---- output raster assembly (output_reducer -> data2raster, utils.py:414-440) ----------------- */
+enum { LT_RASTER_REFERENCE = 0, /* the reference's file: holder cast, then GDT_Byte (App. B #5)   */
+       LT_RASTER_TYPED = 1 };   /* the corrected file: each value in out_type, fill elsewhere      */
+enum { LT_SEL_ALL = 0, LT_SEL_NONZERO = 1, LT_SEL_EQUALS = 2 };
+/* One output key's raster from a plane in device memory. A grid point p contributes when the
+ * selector holds (the reducer emitted the key for it: matched[r][p] != 0 for '<rule>_<field>',
+ * winner[y][p] == obs id for 'trendline/<date>-<attr>'); raster pixel dest[p] then holds its value
+ * (the reference's holder[y_off, x_off] = float(value)), every other pixel NODATA. */
+typedef struct {
+  int64_t n_pix;              /* grid points                                                 */
+  const void* plane;          /* [n_pix] device values, or NULL: const_value for every point */
+  int32_t plane_type;         /* LT_T_I32 / LT_T_F64 / LT_T_U8 / LT_T_I16                     */
+  int32_t sel_kind;           /* LT_SEL_*                                                    */
+  const void* sel;            /* [n_pix] device: uint8 (NONZERO) or int16 (EQUALS) plane      */
+  int32_t sel_value;          /* EQUALS: the obs id                                          */
+  int32_t holder_type;        /* REFERENCE: LT_T_* of the holder (template type promoted)    */
+  double const_value;         /* plane == NULL: the value (class_val: rule.val)              */
+  const int64_t* dest;        /* [n_pix] device raster offsets, all distinct; NULL: dest[p]=p */
+  int64_t n_out;              /* raster pixels (rows * cols)                                 */
+  int32_t mode;               /* LT_RASTER_*                                                 */
+  int32_t out_type;           /* REFERENCE: LT_T_U8; TYPED: LT_T_I32 / LT_T_F64 / LT_T_U8     */
+  double fill;                /* TYPED: value of the pixels no selected point reaches        */
+  void* out;                  /* [n_out] device                                              */
+} lt_raster_job;
+
 typedef struct lt_ctx lt_ctx;
 
 int lt_abi_version(void);
@@ -240,6 +265,17 @@ int lt_analyze_tiles_after(lt_ctx* ctx, const lt_scene* scene, const lt_params* 
  * rule planes of `out` and out->status (only LT_ST_PRE_THRESHOLD_ATTR can be set). */
 int lt_label_tile(lt_ctx* ctx, const lt_label_in* in, const lt_params* params,
                   const lt_tile_out* out, void* stream);
+
+/* Output raster assembly: n_jobs rasters (lt_raster_job), asynchronous on `stream`: a fill of
+ * every raster pixel with NODATA's converted value, then the selected grid points scattered in
+ * (one pass when dest is NULL). Replaces data2raster's per-point loop (utils.py:429-438) and the
+ * holder -> GDT_Byte conversion GDAL does in array2raster (utils.py:374-412). */
+int lt_raster_assemble(lt_ctx* ctx, const lt_raster_job* jobs, int n_jobs, void* stream);
+/* Which observations won some pixel's year (the acquisition dates that get trendline keys,
+ * classes.py:100-116): bit o of bits[] (device, (n_obs + 31) / 32 words, zeroed by the call) is
+ * set iff winner[y * stride + p] == o for some y < n_years, p < n_pix. Asynchronous on `stream`. */
+int lt_winner_presence(lt_ctx* ctx, const int16_t* winner, int64_t stride, int32_t n_years,
+                       int64_t n_pix, int32_t n_obs, uint32_t* bits, void* stream);
 
 /* Stage timing: when enabled, each lt_analyze_tile brackets its kernels with hipEvents on the
  * launch stream; lt_ctx_stage_ms returns the accumulated milliseconds per stage

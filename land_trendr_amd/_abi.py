@@ -87,6 +87,19 @@ EXC_TYPES = {LT_EXC_VALUE: ValueError, LT_EXC_KEY: KeyError, LT_EXC_TYPE: TypeEr
              LT_EXC_OTHER: Exception}
 
 
+LT_RASTER_REFERENCE, LT_RASTER_TYPED = 0, 1
+LT_SEL_ALL, LT_SEL_NONZERO, LT_SEL_EQUALS = 0, 1, 2
+
+
+class LtRasterJob(ctypes.Structure):
+    _fields_ = [('n_pix', ctypes.c_int64), ('plane', ctypes.c_void_p),
+                ('plane_type', ctypes.c_int32), ('sel_kind', ctypes.c_int32),
+                ('sel', ctypes.c_void_p), ('sel_value', ctypes.c_int32),
+                ('holder_type', ctypes.c_int32), ('const_value', ctypes.c_double),
+                ('dest', ctypes.c_void_p), ('n_out', ctypes.c_int64), ('mode', ctypes.c_int32),
+                ('out_type', ctypes.c_int32), ('fill', ctypes.c_double), ('out', ctypes.c_void_p)]
+
+
 class LtIndexIO(ctypes.Structure):
     _fields_ = [('n_pix', ctypes.c_int64), ('n_obs', ctypes.c_int64),
                 ('obs_stride', ctypes.c_int64), ('band_stride', ctypes.c_int64),
@@ -121,7 +134,7 @@ PIX_FIELDS = [('status', 'int32'), ('n_years', 'int32')]
 EXPORTS = ['lt_abi_version', 'lt_ctx_create', 'lt_ctx_destroy', 'lt_last_error',
            'lt_analyze_tile', 'lt_analyze_tiles', 'lt_analyze_tiles_after', 'lt_label_tile', 'lt_ctx_set_timing', 'lt_ctx_stage_ms',
            'lt_ctx_last_deferred', 'lt_index_codegen', 'lt_index_compile', 'lt_index_apply',
-           'lt_settings_compile']
+           'lt_settings_compile', 'lt_raster_assemble', 'lt_winner_presence']
 
 _LIB = None
 
@@ -161,6 +174,9 @@ def load_lib(path=None):
     lib.lt_index_codegen.restype = ctypes.c_int
     lib.lt_index_compile.argtypes = [vp, ctypes.POINTER(LtIndexProg), ctypes.POINTER(vp)]
     lib.lt_index_apply.argtypes = [vp, vp, ctypes.POINTER(LtIndexIO), vp]
+    lib.lt_raster_assemble.argtypes = [vp, ctypes.POINTER(LtRasterJob), ctypes.c_int, vp]
+    lib.lt_winner_presence.argtypes = [vp, vp, ctypes.c_int64, ctypes.c_int32, ctypes.c_int64,
+                                       ctypes.c_int32, vp, vp]
     lib.lt_settings_compile.argtypes = [ctypes.c_char_p, ctypes.c_int32, ctypes.c_int32,
                                         ctypes.c_int32, ctypes.c_int32,
                                         ctypes.POINTER(LtSettings),

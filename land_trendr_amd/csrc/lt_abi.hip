@@ -16,6 +16,7 @@
 #include "lt_pixel.h"
 #include "lt_index.h"
 #include "lt_settings.h"
+#include "lt_raster.h"
 
 namespace {
 
@@ -138,6 +139,48 @@ __global__ __launch_bounds__(kBlock) void label_kernel(const YearArg yrs, int Y,
 struct EventPair {
   hipEvent_t start, stop;
 };
+
+// output raster assembly (lt_raster.h): fill every raster pixel, then scatter the selected grid
+// points; with identity offsets one pass writes both. Grid-stride, coalesced in the pixel index.
+__global__ __launch_bounds__(kBlock) void raster_fill_kernel(const lt_raster_job J) {
+  const double nodata = J.mode == LT_RASTER_REFERENCE ? (double)LT_NODATA : J.fill;
+  for (int64_t o = (int64_t)blockIdx.x * kBlock + threadIdx.x; o < J.n_out;
+       o += (int64_t)gridDim.x * kBlock)
+    lt::raster_store(J, o, nodata);
+}
+
+// presence bitmap of winning obs ids: per block in LDS, then one global OR per word
+__global__ __launch_bounds__(kBlock) void winner_presence_kernel(const int16_t* __restrict__ w,
+                                                                 int64_t stride, int Y,
+                                                                 int64_t n_pix, int n_obs,
+                                                                 uint32_t* __restrict__ bits) {
+  __shared__ uint32_t loc[LT_MAX_OBS / 32];
+  const int nw = (n_obs + 31) / 32;
+  for (int k = threadIdx.x; k < nw; k += kBlock) loc[k] = 0u;
+  __syncthreads();
+  for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < n_pix;
+       p += (int64_t)gridDim.x * kBlock)
+    for (int y = 0; y < Y; y++) {
+      const int o = w[(int64_t)y * stride + p];
+      if (o >= 0 && o < n_obs) atomicOr(&loc[o >> 5], 1u << (o & 31));
+    }
+  __syncthreads();
+  for (int k = threadIdx.x; k < nw; k += kBlock)
+    if (loc[k]) atomicOr(&bits[k], loc[k]);
+}
+
+__global__ __launch_bounds__(kBlock) void raster_scatter_kernel(const lt_raster_job J,
+                                                                bool fill_too) {
+  const double nodata = J.mode == LT_RASTER_REFERENCE ? (double)LT_NODATA : J.fill;
+  for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < J.n_pix;
+       p += (int64_t)gridDim.x * kBlock) {
+    const bool sel = lt::raster_selected(J, p);
+    if (!sel && !fill_too) continue;
+    const double v = !sel ? nodata
+                          : (J.plane ? lt::plane_value(J.plane, J.plane_type, p) : J.const_value);
+    lt::raster_store(J, J.dest ? J.dest[p] : p, v);
+  }
+}
 
 }  // namespace
 
@@ -504,6 +547,66 @@ int lt_ctx_last_deferred(lt_ctx* c, int64_t* n_deferred) {
   HIP_OR_FAIL(c, hipDeviceSynchronize());  // the counters of the last tile's set
   HIP_OR_FAIL(c, hipMemcpy(v, c->d_ndefer + 4 * c->last_set, sizeof v, hipMemcpyDeviceToHost));
   *n_deferred = (int64_t)(v[0] + v[2]);
+  return LT_OK;
+}
+
+int lt_raster_assemble(lt_ctx* c, const lt_raster_job* jobs, int n_jobs, void* stream_) {
+  if (!c) return LT_ERR_ARG;
+  if (n_jobs < 0 || (n_jobs > 0 && !jobs)) return fail(c, LT_ERR_ARG, "null argument%s");
+  for (int k = 0; k < n_jobs; k++) {
+    const lt_raster_job& J = jobs[k];
+    if (J.n_pix < 0 || J.n_out < 0 || (!J.out && J.n_out > 0))
+      return fail(c, LT_ERR_ARG, "bad raster job sizes%s");
+    if (!J.dest && J.n_out != J.n_pix)
+      return fail(c, LT_ERR_ARG, "identity offsets need n_out == n_pix%s");
+    if (J.sel_kind < LT_SEL_ALL || J.sel_kind > LT_SEL_EQUALS || (J.sel_kind != LT_SEL_ALL && !J.sel))
+      return fail(c, LT_ERR_ARG, "bad selector%s");
+    if (J.plane && J.plane_type != LT_T_I32 && J.plane_type != LT_T_F64 &&
+        J.plane_type != LT_T_U8 && J.plane_type != LT_T_I16)
+      return fail(c, LT_ERR_ARG, "bad plane type%s");
+    if (J.mode == LT_RASTER_REFERENCE ? (J.out_type != LT_T_U8 || !lt_idx::ctype(J.holder_type))
+                                      : (J.mode != LT_RASTER_TYPED ||
+                                         (J.out_type != LT_T_I32 && J.out_type != LT_T_F64 &&
+                                          J.out_type != LT_T_U8)))
+      return fail(c, LT_ERR_ARG, "bad raster mode / type%s");
+  }
+  HIP_OR_FAIL(c, hipSetDevice(c->device));
+  hipStream_t st = (hipStream_t)stream_;
+  for (int k = 0; k < n_jobs; k++) {
+    const lt_raster_job& J = jobs[k];
+    auto grid = [](int64_t n) {
+      const int64_t b = (n + kBlock - 1) / kBlock;
+      return dim3((unsigned)(b < 65536 ? (b > 0 ? b : 1) : 65536));
+    };
+    if (J.dest) {
+      if (J.n_out > 0)
+        hipLaunchKernelGGL(raster_fill_kernel, grid(J.n_out), dim3(kBlock), 0, st, J);
+      if (J.n_pix > 0)
+        hipLaunchKernelGGL(raster_scatter_kernel, grid(J.n_pix), dim3(kBlock), 0, st, J, false);
+    } else if (J.n_pix > 0) {
+      hipLaunchKernelGGL(raster_scatter_kernel, grid(J.n_pix), dim3(kBlock), 0, st, J, true);
+    }
+    HIP_OR_FAIL(c, hipGetLastError());
+  }
+  return LT_OK;
+}
+
+int lt_winner_presence(lt_ctx* c, const int16_t* winner, int64_t stride, int32_t n_years,
+                       int64_t n_pix, int32_t n_obs, uint32_t* bits, void* stream_) {
+  if (!c) return LT_ERR_ARG;
+  if (n_years < 0 || n_years > LT_MAX_YEARS || n_obs < 0 || n_obs > LT_MAX_OBS || n_pix < 0 ||
+      stride < n_pix)
+    return fail(c, LT_ERR_ARG, "bad presence sizes%s");
+  if (n_obs == 0) return LT_OK;
+  if (!bits || (n_years > 0 && n_pix > 0 && !winner)) return fail(c, LT_ERR_ARG, "null argument%s");
+  HIP_OR_FAIL(c, hipSetDevice(c->device));
+  hipStream_t st = (hipStream_t)stream_;
+  HIP_OR_FAIL(c, hipMemsetAsync(bits, 0, sizeof(uint32_t) * ((n_obs + 31) / 32), st));
+  if (n_years == 0 || n_pix == 0) return LT_OK;
+  const int64_t b = (n_pix + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL(winner_presence_kernel, dim3((unsigned)(b < 4096 ? b : 4096)), dim3(kBlock), 0,
+                     st, winner, stride, (int)n_years, n_pix, (int)n_obs, bits);
+  HIP_OR_FAIL(c, hipGetLastError());
   return LT_OK;
 }
 

@@ -56,6 +56,35 @@ __device__ inline int lsq_lockstep(bool act, int m, GX X, GY Y, const lsq_xf* __
   return act ? lsq_apply(f, X, Y, need_solution, need_ssr, slope, icpt, ssr) : 0;
 }
 
+// The vertex fits' least squares (solution only), in lockstep: one x-set lookup (lsq_factor for
+// the lanes that miss), then the straight-line lsq_apply_small for the lanes whose segment has
+// 2-4 points — nearly all of them — and the general lsq_apply for the rare longer ones, a branch
+// the wave takes only if some lane needs it.
+template <class GX, class GY>
+__device__ inline int lsq_fit_lockstep(bool act, int m, GX X, GY Y,
+                                       const lsq_xf* __restrict__ xtab, double& slope,
+                                       double& icpt) {
+  const int key = act ? xset_key(m, X) : 0;
+  const bool miss = act && key < 0;
+  lsq_xf f;
+  if (act && !miss) f = xtab[key];
+  if (__ballot(miss)) {
+    if (miss) lsq_factor(m, X, f);
+  }
+  slope = 0.0;
+  icpt = 0.0;
+  int rc = 0;
+  const bool big = act && m > 4;
+  if (__ballot(big)) {
+    if (big) {
+      double ssr;
+      rc = lsq_apply(f, X, Y, true, false, slope, icpt, ssr);
+    }
+  }
+  if (act && m <= 4) rc = lsq_apply_small(f, X, Y, slope, icpt);
+  return rc;
+}
+
 // VT: storage type of the series. The analyze stage stores binary32 (pixels whose values are not
 // exact in binary32 are sent to the resolve stage), the resolve stage binary64.
 // AGLDS: the DP argmin of each column in LDS (resolve stage: its registers are spent on the exact
@@ -77,10 +106,13 @@ struct WaveLds {
 enum { kDone = 0, kDeferExact = 1, kDeferWide = 2 };
 
 // Phase probe of analyze_fast: probe.mark(k) is called by every lane at the end of phase k
-// (0 winner pick, 1 despike, 2 DP, 3 vertex fits + per-year walk + rule offers, 4 label writes).
-// The product kernels pass NoProbe, whose mark compiles to nothing; profiles/stamp_probe.h
-// defines the cycle-stamping probe of the profiling build (profiles/stamps.sh).
+// (0 winner pick, 1 despike, 2 DP, 3 vertex fits + per-year walk + rule offers, 4 label writes),
+// and a probe whose kStopAfter is k ends the pixel there. The product kernels pass NoProbe (mark
+// compiles to nothing, kStopAfter = -1 removes the exits); the profiling builds of profiles/
+// (stamps.sh: cycle stamps; phases.sh: PMC counts of the kernel cut after each phase) define the
+// others.
 struct NoProbe {
+  static constexpr int kStopAfter = -1;
   __device__ void mark(int) const {}
 };
 
@@ -178,6 +210,7 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
     }
   }
   probe.mark(0);
+  if constexpr (Probe::kStopAfter == 0) return kDone;
   // the reference raises for T < 2; non-binary32 values take the resolve stage's double path
   const bool ok = live && T >= 2 && !f32_bad;
   if (live && T == 0) status |= LT_ST_EMPTY;
@@ -276,6 +309,7 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
     }
   }
   probe.mark(1);
+  if constexpr (Probe::kStopAfter == 1) return kDone;
   const int nmax = wave_max(n);
 
   // ---- segmented least squares DP (utils.py:618-631), decided lazily ----
@@ -681,6 +715,7 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
     }
   }
   probe.mark(2);
+  if constexpr (Probe::kStopAfter == 2) return kDone;
   // deferred lanes stay in the wave (the loops below use wave collectives) but do nothing more
   if (deferred) vmask = 0;
 
@@ -708,11 +743,11 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
     // vertex reuse the previous equation, utils.py:662)
     const int mseg = has_next ? kb - ka + 1 : 2;
     const int kbase = has_next ? ka : 0;
-    double sm = 0.0, sbv = 0.0, ssr = 0.0;
+    double sm = 0.0, sbv = 0.0;
     if (__ballot(has_next)) {
-      const int rc = lsq_lockstep(
+      const int rc = lsq_fit_lockstep(
           has_next, mseg, [&](int k) { return (int)L.xn[kbase + k][lane]; },
-          [&](int k) { return (double)L.ys[kbase + k][lane]; }, xtab, true, false, sm, sbv, ssr);
+          [&](int k) { return (double)L.ys[kbase + k][lane]; }, xtab, sm, sbv);
       if (has_next) {
         if (rc < 0) status |= LT_ST_NUMERIC;
         cm = sm;
@@ -791,6 +826,7 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
   }
 
   probe.mark(3);
+  if constexpr (Probe::kStopAfter == 3) return kDone;
   // ---- change_labeling (utils.py:795-820) outputs ----
   if (live && !deferred) {
 #pragma unroll

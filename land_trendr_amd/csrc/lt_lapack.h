@@ -833,6 +833,68 @@ __host__ __device__ inline int lsq_apply(const lsq_xf& f, GX X, GY Y, bool need_
   return rank == 2 ? 0 : -3;
 }
 
+// lsq_apply's solution for 2 <= m <= 4 as straight-line code: the same operations in the same
+// order (pass A's four interleaved sums or its FMA tail, B = H1 y, pass C's gemv_t1 over
+// lastv2 <= 3 elements, DLALSD's solve), with m selecting between them instead of loops and
+// branches on per-lane counts, so a wave whose lanes fit segments of different short lengths
+// runs one short sequence. The vertex fits (vertices2eqns, utils.py:646-669) are nearly all
+// 2-4 points long. tests/test_lapack_emulation.py checks it against lsq_apply bit for bit.
+template <class GX, class GY>
+__host__ __device__ inline int lsq_apply_small(const lsq_xf& f, GX X, GY Y, double& slope,
+                                               double& icpt) {
+  slope = 0.0;
+  icpt = 0.0;
+  if (f.rc < 0) return f.rc;
+  const int m = f.m;
+  const double s1 = f.s1;
+  const bool m3p = m >= 3, m4 = m >= 4;
+  const double y0 = Y(0), y1 = Y(1), y2 = m3p ? Y(2) : 0.0, y3 = m4 ? Y(3) : 0.0;
+  const double t1 = (double)X(1) * s1;
+  const double t2 = m3p ? (double)X(2) * s1 : 0.0;
+  const double t3 = m4 ? (double)X(3) * s1 : 0.0;
+  // pass A, y half (lsq_apply: m1 = 4 for m = 4, else the FMA tail)
+  double wy;
+  if (m4) {
+    const double Q0 = 0.0 + y0 * 1.0, Q1 = 0.0 + y1 * t1, Q2 = 0.0 + y2 * t2, Q3 = 0.0 + y3 * t3;
+    wy = __builtin_fma((Q0 + Q2) + (Q1 + Q3), 1.0, 0.0);
+  } else {
+    const double inner = __builtin_fma(y0, 1.0, y1 * t1);
+    wy = 0.0 + (m3p ? __builtin_fma(y2, t2, inner) : inner);
+  }
+  const double bmax = __builtin_fmax(__builtin_fmax(__builtin_fabs(y0), __builtin_fabs(y1)),
+                                     __builtin_fmax(__builtin_fabs(y2), __builtin_fabs(y3)));
+  if (bmax == 0.0) return 0;  // DGELSD: B == 0 -> zero solution
+  if (!(bmax >= 0x1p-970 && bmax <= 0x1p970)) return -1;
+  const double sb = f.ntau1 * wy;
+  const double B0 = __builtin_fma(sb, 1.0, y0), B1 = __builtin_fma(sb, t1, y1);
+  double b1 = B1;
+  if (m3p) {
+    const double B2 = __builtin_fma(sb, t2, y2), B3 = __builtin_fma(sb, t3, y3);
+    if (f.tau2nz) {  // pass C: gemv_t1(lastv2, B(k+1), v2) and DLARF's "any nonzero" test
+      const double sc = f.sc, s2 = f.s2;
+      const int lv = f.lastv2;
+      const double v21 = __builtin_fma(sc, t2, 1.0) * s2;
+      const double v22 = m4 ? __builtin_fma(sc, t3, 1.0) * s2 : 0.0;
+      double w2;
+      bool any;
+      if (lv == 1) {
+        w2 = __builtin_fma(B1, 1.0, 0.0);
+        any = B1 != 0.0;
+      } else if (lv == 2) {
+        w2 = 0.0 + __builtin_fma(B1, 1.0, B2 * v21);
+        any = B1 != 0.0 || B2 != 0.0;
+      } else {
+        w2 = 0.0 + __builtin_fma(B3, v22, __builtin_fma(B1, 1.0, B2 * v21));
+        any = B1 != 0.0 || B2 != 0.0 || B3 != 0.0;
+      }
+      if (any) b1 = __builtin_fma(f.ntau2 * w2, 1.0, B1);
+    }
+  }
+  if (f.R.rank < 0) return -1;
+  dlalsd2_b(f.R, B0, b1, slope, icpt);
+  return f.R.rank == 2 ? 0 : -3;
+}
+
 template <class GX, class GY>
 __host__ __device__ inline int lstsq_xint(int m, GX X, GY Y, bool need_solution, bool need_ssr,
                                           double& slope, double& icpt, double& ssr) {

@@ -197,6 +197,18 @@ class Engine:
                                             ctypes.c_void_p(st.cuda_stream)), 'lt_index_apply')
         return out
 
+    # --- output raster assembly (output_reducer -> data2raster, lt_raster_assemble) ---
+    def raster_assemble(self, jobs, stream=None):
+        """jobs: a list of _abi.LtRasterJob (device pointers of this engine's tensors, which the
+        caller keeps alive until the stream has run them)."""
+        if not jobs:
+            return
+        arr = (_abi.LtRasterJob * len(jobs))(*jobs)
+        st = stream if stream is not None else torch.cuda.current_stream(self.device)
+        self._check(self.lib.lt_raster_assemble(self.ctx, arr, len(jobs),
+                                                ctypes.c_void_p(st.cuda_stream)),
+                    'lt_raster_assemble')
+
     # --- stage timing (HIP events recorded around every launch on the launch stream) ---
     def set_timing(self, enable):
         self._check(self.lib.lt_ctx_set_timing(self.ctx, 1 if enable else 0), 'set_timing')

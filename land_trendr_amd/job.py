@@ -134,16 +134,27 @@ class LocalJob:
         runner = MosaicRunner(eng, m, params, items, fields, fn, dist, exchange_fields=fields)
         runner.step()
         torch.cuda.synchronize(dev)
+        self._host = None
         if not runner.exchange.is_writer:
-            self.planes = None
+            self.dev_planes = None
             return None
-        self.planes = {f: runner.exchange.raster(f).cpu().numpy() for f in fields}
+        # the writer's planes stay in HBM: the output step assembles each raster there
+        self.dev_planes = {f: runner.exchange.raster(f) for f in fields}
+        self.engine = eng
         self._check_errors()
-        return self.planes
+        return self.dev_planes
+
+    @property
+    def planes(self):
+        """Host copies of the writer's output planes (made on first use)."""
+        if self._host is None and self.dev_planes is not None:
+            self._host = {f: t.cpu().numpy() for f, t in self.dev_planes.items()}
+        return self._host
 
     def _check_errors(self):
+        import torch
         from .utils import _raise_for_status
-        status = self.planes['status']
+        status = self.dev_planes['status'].cpu().numpy()
         bad = np.flatnonzero(status & ~_abi.LT_ST_EMPTY)
         if len(bad) == 0:
             return
@@ -159,14 +170,23 @@ class LocalJob:
             except Exception as e:
                 raise type(e)('%s (pixel %s)' % (e, wkt)) from e
         else:  # skip: the failing pixels emit nothing
-            self.planes['matched'][:, bad] = 0
-            if 'winner' in self.planes:
-                self.planes['winner'][:, bad] = -1
+            idx = torch.from_numpy(bad).to(self.dev_planes['matched'].device)
+            self.dev_planes['matched'][:, idx] = 0
+            if 'winner' in self.dev_planes:
+                self.dev_planes['winner'][:, idx] = -1
+            self._host = None
 
     # 4. output_reducer
     def output(self):
+        """Every output key's raster, written as LZW GeoTIFF with the template's georeferencing.
+        With one grid point per raster pixel (the co-registered grid setup builds) the rasters
+        are assembled on the GPU (lt_raster_assemble) and each one reaches the host only as its
+        finished GDT_Byte (or typed) array, written at once; a grid that maps two points to one
+        pixel (the reference's loop: the last one wins) is assembled on the host."""
+        import torch
         from .geotiff import GeoTiff
-        from .raster import label_rasters, output_reducer, trendline_rasters
+        from .raster import (label_rasters, label_rasters_device, output_reducer,
+                             trendline_rasters, trendline_rasters_device)
         tmpl = GeoTiff(self.rast_fns[0])
         rows, cols = tmpl.height, tmpl.width
         lng, lat = grid_points(self.grid_fn)
@@ -175,18 +195,34 @@ class LocalJob:
             # data2raster assigns holder[y_off, x_off]: an off-template point raises there
             raise IndexError('grid point %s is off the template raster'
                              % read_grid(self.grid_fn)[int(np.flatnonzero(~ok)[0])])
+        tdt = tmpl.dtype.newbyteorder('=')
+        dp = self.dev_planes
+        # an EMPTY pixel never reaches the reference's reducer: it emits nothing
+        empty = (dp['status'] & _abi.LT_ST_EMPTY) != 0
+        dp['matched'].masked_fill_(empty[None, :], 0)
+        self._host = None
+        names = [d.strftime('%Y-%m-%d') for d in self.scene.dates]
+        if len(np.unique(dest)) == len(dest) and len(set(names)) == len(names):
+            ddest = torch.from_numpy(np.ascontiguousarray(dest, np.int64)).to(dp['status'].device)
+            out = {}
+
+            def write(key, arr):  # each raster to its file as soon as it is on the host
+                out.update(output_reducer({key: arr}, tmpl, self.root, self.job))
+
+            for k, a in label_rasters_device(self.engine, dp, self.rules, (rows, cols), ddest,
+                                             tdt, self.raster_mode).items():
+                write(k, a)
+            if self.trendline:
+                trendline_rasters_device(self.engine, dp, self.scene, self.scene.dates,
+                                         (rows, cols), ddest, tdt, self.raster_mode, sink=write)
+            return out
         n = rows * cols
         placed = {}
-        empty = self.planes['status'] & _abi.LT_ST_EMPTY
         for k, a in self.planes.items():
             fill = -1 if k == 'winner' else 0
             b = np.full(a.shape[:-1] + (n,), fill, a.dtype)
-            src = a
-            if k == 'matched':
-                src = np.where(empty[None, :] != 0, 0, a).astype(a.dtype)
-            b[..., dest] = src  # repeated offsets: the last grid point wins, as in the loop
+            b[..., dest] = a  # repeated offsets: the last grid point wins, as in the loop
             placed[k] = b
-        tdt = tmpl.dtype.newbyteorder('=')
         rasters = label_rasters(placed, self.rules, (rows, cols), tdt, self.raster_mode)
         if self.trendline:
             rasters.update(trendline_rasters(placed, self.scene, self.scene.dates, (rows, cols),

@@ -74,8 +74,8 @@ def label_rasters(out, rules, shape, template_dtype=np.int16, mode='reference'):
         m = matched[r, :rows * cols].reshape(rows, cols).astype(bool)
         for key in LABEL_KEYS:
             plane = _np(out[key])[r, :rows * cols].reshape(rows, cols)
-            if key == 'class_val':
-                plane = np.full(plane.shape, rule.val, np.int32)
+            if key == 'class_val':  # the reducer emits rule.val; data2raster takes float(value)
+                plane = np.full(plane.shape, float(rule.val))
             if mode == 'typed':
                 typ = np.float64 if key == 'magnitude' else np.int32
                 res['%s_%s' % (rule.name, key)] = np.where(m, plane, NODATA).astype(typ)
@@ -254,3 +254,109 @@ def output_reducer(rasters, template, out_dir, job='job', compress='lzw'):
         os.makedirs(os.path.dirname(path), exist_ok=True)
         write_geotiff(path, rasters[key], template=tmpl, compress=compress)
         yield key, [path]
+
+
+# ---- the same rasters assembled on the GPU (lt_raster_assemble) --------------------------------
+def _job(n_pix, n_out, plane, sel_kind, sel, sel_value, holder_t, const_value, dest, mode,
+         out_type, out):
+    from . import engine as _eng
+    j = _abi.LtRasterJob()
+    j.n_pix, j.n_out = n_pix, n_out
+    if plane is not None:
+        j.plane, j.plane_type = plane.data_ptr(), _eng._LT_T[plane.dtype]
+    j.sel_kind, j.sel, j.sel_value = sel_kind, sel.data_ptr() if sel is not None else None, \
+        int(sel_value)
+    j.holder_type = holder_t
+    j.const_value = float(const_value)
+    j.dest = dest.data_ptr() if dest is not None else None
+    j.mode, j.out_type, j.fill, j.out = mode, out_type, float(NODATA), out.data_ptr()
+    return j
+
+
+def label_rasters_device(engine, planes, rules, shape, dest=None, template_dtype=np.int16,
+                         mode='reference'):
+    """label_rasters for [R, P] planes in device memory (matched, onset_year, duration,
+    magnitude): each '<rule>_<field>' raster is assembled by lt_raster_assemble and only the
+    finished raster is copied to the host. dest: None (grid point p is raster pixel p) or a device
+    int64 [P] of distinct raster offsets. Same values as label_rasters on the host planes."""
+    import torch
+    from .index_eqn import DTYPES
+    rows, cols = shape
+    n_out = rows * cols
+    P = planes['matched'].shape[-1]
+    ref = mode == 'reference'
+    hdt = DTYPES[holder_dtype(template_dtype)] if ref else 0
+    jobs, res = [], {}
+    for r, rule in enumerate(rules):
+        sel = planes['matched'][r]
+        for key in LABEL_KEYS:
+            typ = torch.uint8 if ref else (torch.float64 if key == 'magnitude' else torch.int32)
+            out = torch.empty(n_out, dtype=typ, device=engine.device)
+            plane = None if key == 'class_val' else planes[key][r]
+            jobs.append(_job(P, n_out, plane, _abi.LT_SEL_NONZERO, sel, 0, hdt,
+                             float(rule.val) if key == 'class_val' else 0.0, dest,
+                             _abi.LT_RASTER_REFERENCE if ref else _abi.LT_RASTER_TYPED,
+                             {torch.uint8: _abi.LT_T_U8, torch.int32: _abi.LT_T_I32,
+                              torch.float64: _abi.LT_T_F64}[typ], out))
+            res['%s_%s' % (rule.name, key)] = out
+    engine.raster_assemble(jobs)
+    return {k: v.cpu().numpy().reshape(rows, cols) for k, v in res.items()}
+
+
+def trendline_rasters_device(engine, planes, scene, dates, shape, dest=None,
+                             template_dtype=np.int16, mode='reference', attrs=TRENDLINE_ATTRS,
+                             sink=None):
+    """trendline_rasters for [Y, P] planes in device memory: the winning acquisition dates come
+    from lt_winner_presence, each 'trendline/<date>-<attr>' raster from lt_raster_assemble, one
+    year slot at a time; sink(key, array) receives each raster as it reaches the host (default:
+    collected into the returned dict). Dates shared by two observations fall back to the host."""
+    import ctypes
+    import torch
+    from .index_eqn import DTYPES
+    rows, cols = shape
+    n_out = rows * cols
+    w = planes['winner']
+    Y, P = w.shape
+    K = scene.n_obs
+    names = [d.strftime('%Y-%m-%d') for d in dates]
+    if len(set(names)) != len(names):
+        raise ValueError('two observations share an acquisition date: assemble on the host')
+    bits = torch.zeros((K + 31) // 32, dtype=torch.int32, device=engine.device)
+    st = torch.cuda.current_stream(engine.device)
+    engine._check(engine.lib.lt_winner_presence(engine.ctx, w.data_ptr(), w.stride(0), Y, P, K,
+                                                bits.data_ptr(), ctypes.c_void_p(st.cuda_stream)),
+                  'lt_winner_presence')
+    b = bits.cpu().numpy().view(np.uint32)
+    present = [o for o in range(K) if (b[o >> 5] >> (o & 31)) & 1]
+    slot_of = {}
+    for y in range(scene.n_years):
+        for k in range(scene.slot_begin[y], scene.slot_begin[y + 1]):
+            slot_of[int(scene.order[k])] = y
+    ref = mode == 'reference'
+    hdt = DTYPES[holder_dtype(template_dtype)] if ref else 0
+    res = {}
+    for o in present:
+        y = slot_of[o]
+        jobs, outs = [], []
+        for a in attrs:
+            plane = planes[_PLANE_OF_ATTR[a]][y]
+            if ref:
+                typ, ot = torch.uint8, _abi.LT_T_U8
+            else:
+                typ, ot = ((torch.uint8, _abi.LT_T_U8) if a in ('spike', 'vertex') else
+                           (torch.float64, _abi.LT_T_F64))
+            out = torch.empty(n_out, dtype=typ, device=engine.device)
+            j = _job(P, n_out, plane, _abi.LT_SEL_EQUALS, w[y], o, hdt, 0.0, dest,
+                     _abi.LT_RASTER_REFERENCE if ref else _abi.LT_RASTER_TYPED, ot, out)
+            if not ref and a in ('spike', 'vertex'):
+                j.fill = 0.0
+            jobs.append(j)
+            outs.append(('trendline/%s-%s' % (names[o], a), out))
+        engine.raster_assemble(jobs)
+        for key, out in outs:
+            arr = out.cpu().numpy().reshape(rows, cols)
+            if sink is not None:
+                sink(key, arr)
+            else:
+                res[key] = arr
+    return res

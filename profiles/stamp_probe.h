@@ -8,6 +8,7 @@
 __device__ unsigned long long lt_stamp_cycles[8];
 
 struct StampProbe {
+  static constexpr int kStopAfter = -1;
   mutable unsigned long long t;
   __device__ StampProbe() : t(__builtin_amdgcn_s_memtime()) {}
   __device__ void mark(int k) const {

@@ -98,3 +98,21 @@ extern "C" int ltx_xset_roundtrip(int* n_valid) {
   *n_valid = nv;
   return bad;
 }
+
+// lsq_apply_small (the vertex fits' straight-line path, m <= 4) against lsq_apply on the same
+// factorisation: out4 = {small slope, small intercept, general slope, general intercept};
+// returns the two return codes packed as small * 16 + general (each offset by 8)
+extern "C" int ltx_lsq_small_vs_general(int m, const double* x, const double* y, double* out4) {
+  lt::lsq_xf f;
+  auto X = [&](int k) { return (int)x[k]; };
+  auto Y = [&](int k) { return y[k]; };
+  lt::lsq_factor(m, X, f);
+  double s0, c0, s1, c1, r1;
+  const int a = lt::lsq_apply_small(f, X, Y, s0, c0);
+  const int b = lt::lsq_apply(f, X, Y, true, false, s1, c1, r1);
+  out4[0] = s0;
+  out4[1] = c0;
+  out4[2] = s1;
+  out4[3] = c1;
+  return (a + 8) * 16 + (b + 8);
+}

@@ -231,3 +231,40 @@ def test_xset_table_keys_round_trip(hc):
     hc.ltx_xset_roundtrip.argtypes = [ctypes.POINTER(ctypes.c_int)]
     assert hc.ltx_xset_roundtrip(ctypes.byref(nv)) == 0
     assert nv.value > 8000
+
+
+def test_small_segment_apply_matches_general_bit_for_bit(hc):
+    """lsq_apply_small (the vertex fits' straight-line path for 2-4 points) gives lsq_apply's
+    solution bits and return code on the same factorisation: integer, non-integer, zero, tiny,
+    huge and collinear y over consecutive and gapped x."""
+    D = ctypes.POINTER(ctypes.c_double)
+    hc.ltx_lsq_small_vs_general.argtypes = [ctypes.c_int, D, D, D]
+    rng = np.random.default_rng(77)
+    out = (ctypes.c_double * 4)()
+    n = 0
+    for t in range(30000):
+        m = 2 + t % 3
+        x = np.cumsum(rng.integers(1, 1 + [1, 3, 9][t % 3], m)).astype(np.float64) + \
+            float(rng.integers(0, 40))
+        kind = (t // 3) % 6
+        if kind == 0:
+            y = rng.integers(-32768, 32768, m).astype(np.float64)
+        elif kind == 1:
+            y = rng.normal(0, 1, m)
+        elif kind == 2:
+            y = np.zeros(m)
+            y[rng.integers(0, m)] = float(rng.integers(-3, 4))
+        elif kind == 3:
+            y = rng.normal(0, 1, m) * 2.0 ** int(rng.integers(-990, 990))
+        elif kind == 4:
+            y = 5.0 + 2.5 * x
+        else:
+            y = np.round(rng.normal(1000, 40, m))
+        rc = hc.ltx_lsq_small_vs_general(m, x.ctypes.data_as(D), y.ctypes.data_as(D),
+                                         ctypes.cast(out, D))
+        a, b = rc // 16 - 8, rc % 16 - 8
+        assert a == b, (m, x, y, a, b)
+        if b == 0:
+            assert golden_io._bits_equal(np.array(out[:2]), np.array(out[2:])).all(), (m, x, y)
+            n += 1
+    assert n > 20000
