@@ -46,19 +46,22 @@ __device__ inline void defer_append(bool deferred, int64_t p, int lane, int64_t*
 #ifndef LT_ANALYZE_PROBE
 #define LT_ANALYZE_PROBE lt::NoProbe
 #endif
-template <int MAXY, int RMAX>
+// VT: the LDS type of the series — int16 when the tile's index raster is int16 (every value fits;
+// half the LDS of binary32, so more waves per CU), else binary32 (values it cannot hold defer the
+// pixel to the binary64 resolve).
+template <int MAXY, int RMAX, class VT>
 __global__ __launch_bounds__(64, (MAXY <= 32 && RMAX == 1) ? LT_FAST_WAVES_C2 : LT_FAST_WAVES_BIG) void analyze_fast_kernel(const lt::DevScene* __restrict__ S,
                                                           const lt_params P, const lt_tile_in in,
                                                           const lt_tile_out out,
                                                           const lt::lsq_xf* __restrict__ xtab,
                                                           int64_t* __restrict__ defer,
                                                           unsigned long long* __restrict__ n_defer) {
-  __shared__ lt::WaveLds<MAXY, float, false> L;
+  __shared__ lt::WaveLds<MAXY, VT, false> L;
   const int lane = threadIdx.x;
   const int64_t p = (int64_t)blockIdx.x * 64 + lane;
   const bool live = p < in.n_pix;
-  const int d = lt::analyze_fast<MAXY, RMAX, false, float>(*S, P, in, out, xtab, p, live, lane, L,
-                                                           LT_ANALYZE_PROBE{});
+  const int d = lt::analyze_fast<MAXY, RMAX, false, VT>(*S, P, in, out, xtab, p, live, lane, L,
+                                                        LT_ANALYZE_PROBE{});
   // two lists: [0, n_pix) for the binary32 resolve, [n_pix, 2 n_pix) for the binary64 one;
   // counters [0] / [2] count them (wave-aggregated atomics)
   defer_append(live && d == lt::kDeferExact, p, lane, defer, &n_defer[0]);
@@ -367,9 +370,16 @@ static int launch_tile(lt_ctx* c, const lt_params* prm, const lt_tile_in* in,
   if (nwave > 0x7fffffff) return fail(c, LT_ERR_LIMIT, "tile too large%s");
   dim3 fgrid((unsigned)nwave), fblock(64);
   const bool one = prm->n_rules <= 1, few = prm->n_rules <= 4;
-#define LT_LAUNCH_FAST(MY, RM)                                                              \
-  hipLaunchKernelGGL((analyze_fast_kernel<MY, RM>), fgrid, fblock, 0, stream, c->d_scene, *prm, \
-                     *in, *out, c->d_xtab, dl, dn)
+  const bool i16 = in->obs_index && in->index_type == LT_T_I16;
+#define LT_LAUNCH_FAST(MY, RM)                                                                 \
+  do {                                                                                     \
+    if (i16)                                                                               \
+      hipLaunchKernelGGL((analyze_fast_kernel<MY, RM, int16_t>), fgrid, fblock, 0, stream,   \
+                         c->d_scene, *prm, *in, *out, c->d_xtab, dl, dn);                  \
+    else                                                                                   \
+      hipLaunchKernelGGL((analyze_fast_kernel<MY, RM, float>), fgrid, fblock, 0, stream,     \
+                         c->d_scene, *prm, *in, *out, c->d_xtab, dl, dn);                  \
+  } while (0)
 #ifdef LT_DEV_ONE_CONFIG  // A/B and assembly builds only: the (MAXY = LT_DEV_ONE_CONFIG, 1 rule)
   (void)one; (void)few;     // instances alone
   LT_LAUNCH_FAST(LT_DEV_ONE_CONFIG, 1);
@@ -400,8 +410,9 @@ static int launch_tile(lt_ctx* c, const lt_params* prm, const lt_tile_in* in,
   } while (0)
 #define LT_LAUNCH_RESOLVE(MY, RM)                                                            \
   do {                                                                                      \
-    LT_LAUNCH_RESOLVE1(MY, RM, float, dl, dn);                             \
-    LT_LAUNCH_RESOLVE1(MY, RM, double, dl + in->n_pix, dn + 2);            \
+    if (i16) LT_LAUNCH_RESOLVE1(MY, RM, int16_t, dl, dn);                                   \
+    else LT_LAUNCH_RESOLVE1(MY, RM, float, dl, dn);                                         \
+    LT_LAUNCH_RESOLVE1(MY, RM, double, dl + in->n_pix, dn + 2);                             \
   } while (0)
 #ifdef LT_DEV_ONE_CONFIG
   LT_LAUNCH_RESOLVE(LT_DEV_ONE_CONFIG, 1);

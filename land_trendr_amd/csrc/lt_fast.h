@@ -19,7 +19,7 @@
 #endif
 // the exact DP keeps OPT in private memory up to this many years, in registers above
 #ifndef LT_RESOLVE_PRIV_MAXY
-#define LT_RESOLVE_PRIV_MAXY 32
+#define LT_RESOLVE_PRIV_MAXY 48
 #endif
 
 namespace lt {
@@ -190,7 +190,7 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
         const double v = val[u];
         if (T == 0) y0 = S.year[y];
         const VT vs = (VT)v;
-        if constexpr (!EXACT || sizeof(VT) == 4) {
+        if constexpr (!EXACT || sizeof(VT) < 8) {
           if (!((double)vs == v)) f32_bad = true;
         }
         L.ys[T][lane] = vs;
