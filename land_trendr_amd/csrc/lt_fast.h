@@ -539,6 +539,7 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
     int xA = 0, xB = 0, xC = 0, xD = 0;
     double yA = 0.0, yB = 0.0, yC = 0.0, yD = 0.0;
     double oA = 0.0, oB = 0.0, oC = 0.0, oD = 0.0;  // oA = OPTa[0] for column 0
+    bool eA = true, eB = true, eC = true, eD = true;  // exactness of the OPTa window slots
     double SyyAll = 0.0;                // sum of y^2 over the points 0..j
     const bool prune = c >= 0.0;
     uint64_t amb = 0;
@@ -546,7 +547,8 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
     // opt_j..opt_jm3 hold OPTa[j..j-3], and OPTa[j+1] is written over opt_jm3
     auto column = [&](const int j, int& wx0, int& wx1, int& wx2, int& wx3, double& wy0,
                       double& wy1, double& wy2, double& wy3, double& opt_j, double& opt_jm1,
-                      double& opt_jm2, double& opt_jm3) __attribute__((always_inline)) {
+                      double& opt_jm2, double& opt_jm3, bool& ex_j, bool& ex_jm1, bool& ex_jm2,
+                      bool& ex_jm3) __attribute__((always_inline)) {
       const bool col = j < n;
       double Sy = 0.0, Sxy = 0.0, Syy = 0.0;
       int Sx = 0, Sxx = 0;
@@ -562,7 +564,7 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
         const int i = j - s;
         if (i < 0) continue;  // wave-uniform
         const double v = c + (s ? opt_jm1 : opt_j);
-        if ((exact >> i) & 1) {
+        if (s ? ex_jm1 : ex_j) {
           if (v <= Ve) {
             Ve = v;
             ie = i;
@@ -592,9 +594,12 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
         Sxy = __builtin_fma((double)xi, yi, Sxy);
         Syy = __builtin_fma(yi, yi, Syy);
       };
+      // the early-exit bound's screening slack, the same for every start of the column
+      const double slack = 4.0 * kScreen * SyyAll * (1.0 + 0x1p-49);
       // start i (>= 3 points) priced from the current sums: value v, its interval [lo, hi] around
-      // the reference value, and the early-exit bound for the starts below it
-      auto price = [&](int i, double o, double& v, double& hi, double& lo, double& bnd) {
+      // the reference value (ex: OPTa[i] is exact), and the early-exit bound for the starts below
+      auto price = [&](int i, double o, bool ex, double& v, double& hi, double& lo,
+                       double& bnd) {
         // closed-form SSE: (m*Syy - Sy^2 - N1^2/D) / m, one reciprocal
         const int m = j - i + 1;  // wave-uniform, >= 3
         const double md = (double)m;
@@ -608,11 +613,11 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
         v = (e + c) + o;  // o = OPTa[i]
         // interval around the reference value: OPT bound + screening bound of this segment +
         // the rounding of this candidate's own two additions
-        const double wopt = ((exact >> i) & 1) ? 0.0 : Emax;
+        const double wopt = ex ? 0.0 : Emax;
         const double w = __builtin_fma(0x1p-50, __builtin_fabs(v), __builtin_fma(kScreen, Syy, wopt));
         hi = v + w;
         lo = v - w;
-        bnd = dp_start_bound(e, o, wopt, c, SyyAll);
+        bnd = dp_start_bound_slack(e, o, wopt, c, slack);
       };
       // candidates in decreasing start order ("<=" keeps the smaller start among equal values)
       auto track = [&](int i, double v, double hi, double lo) {
@@ -638,10 +643,10 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
         const bool two = j >= 3;
         double va, ha, la, ba, vb = 0.0, hb = 0.0, lb = 0.0, bb = 0.0;
         add_xy(wx2, wy2);
-        price(j - 2, opt_jm2, va, ha, la, ba);
+        price(j - 2, opt_jm2, ex_jm2, va, ha, la, ba);
         if (two) {
           add_xy(wx3, wy3);
-          price(j - 3, opt_jm3, vb, hb, lb, bb);
+          price(j - 3, opt_jm3, ex_jm3, vb, hb, lb, bb);
         }
         track(j - 2, va, ha, la);
         if (two) track(j - 3, vb, hb, lb);
@@ -656,10 +661,10 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
         const bool two = i >= 1;                            // wave-uniform
         add_xy(L.xn[i][lane], (double)L.ys[i][lane]);
         double va, ha, la, ba, vb = 0.0, hb = 0.0, lb = 0.0, bb = 0.0;
-        price(i, OPTa[i], va, ha, la, ba);
+        price(i, OPTa[i], (exact >> i) & 1, va, ha, la, ba);
         if (two) {
           add_xy(L.xn[i - 1][lane], (double)L.ys[i - 1][lane]);
-          price(i - 1, OPTa[i - 1], vb, hb, lb, bb);
+          price(i - 1, OPTa[i - 1], (exact >> (i - 1)) & 1, vb, hb, lb, bb);
         }
         track(i, va, ha, la);
         if (two) track(i - 1, vb, hb, lb);
@@ -694,14 +699,18 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
         if (exnew) exact |= 2ull << j;
         Emax = enew > Emax ? enew : Emax;
         opt_jm3 = vnew;  // OPTa[j+1]: the slot of OPTa[j-3], which no later column reads
+        ex_jm3 = exnew;
       }
     };
     for (int jj = 0; jj < nmax; jj += 4) {
       const int j = __builtin_amdgcn_readfirstlane(jj);  // column index in an SGPR
-      column(j, xA, xB, xC, xD, yA, yB, yC, yD, oA, oB, oC, oD);
-      if (j + 1 < nmax) column(j + 1, xD, xA, xB, xC, yD, yA, yB, yC, oD, oA, oB, oC);
-      if (j + 2 < nmax) column(j + 2, xC, xD, xA, xB, yC, yD, yA, yB, oC, oD, oA, oB);
-      if (j + 3 < nmax) column(j + 3, xB, xC, xD, xA, yB, yC, yD, yA, oB, oC, oD, oA);
+      column(j, xA, xB, xC, xD, yA, yB, yC, yD, oA, oB, oC, oD, eA, eB, eC, eD);
+      if (j + 1 < nmax)
+        column(j + 1, xD, xA, xB, xC, yD, yA, yB, yC, oD, oA, oB, oC, eD, eA, eB, eC);
+      if (j + 2 < nmax)
+        column(j + 2, xC, xD, xA, xB, yC, yD, yA, yB, oC, oD, oA, oB, eC, eD, eA, eB);
+      if (j + 3 < nmax)
+        column(j + 3, xB, xC, xD, xA, yB, yC, yD, yA, oB, oC, oD, oA, eB, eC, eD, eA);
     }
     // find_segments (utils.py:633-644): starts of the optimal segments + the last point
     if (n >= 1) {

@@ -190,10 +190,14 @@ __host__ __device__ inline double obs_value(const lt_tile_in& in, int64_t i) {
 // the three residuals involved is within kScreen * its sum(y^2) <= SyyAll of the exact one, and
 // the factors cover the roundings. Once it exceeds an upper bound on the column minimum, no start
 // below i can be (or tie) the minimum.
+__host__ __device__ inline double dp_start_bound_slack(double e, double opta, double eopt,
+                                                       double c, double slack) {
+  const double o = opta - eopt > c ? opta - eopt : c;
+  return (e + o) * (1.0 - 0x1p-49) - slack;
+}
 __host__ __device__ inline double dp_start_bound(double e, double opta, double eopt, double c,
                                                  double SyyAll) {
-  const double o = opta - eopt > c ? opta - eopt : c;
-  return (e + o) * (1.0 - 0x1p-49) - 4.0 * kScreen * SyyAll * (1.0 + 0x1p-49);
+  return dp_start_bound_slack(e, opta, eopt, c, 4.0 * kScreen * SyyAll * (1.0 + 0x1p-49));
 }
 
 // segmented_least_squares' DP (utils.py:618-631) with candidate screening.
