@@ -11,6 +11,8 @@
 //     column without LAPACK emulation whenever the closed-form prices separate (dp_lazy's rule);
 //   * no scratch memory.
 #pragma once
+#include <type_traits>
+
 #include "lt_pixel.h"
 
 // winner-pick batch: year slots whose value loads are issued together
@@ -133,6 +135,7 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
   int T = 0, y0 = 0;
   uint64_t pres = 0;  // year slots with a winner: present point t is the t-th set bit
   bool f32_bad = false;
+  bool intdata = true;  // every value an integer of int16 range (lt_pixel.h sse_exact_zero)
   // years in batches of 8: the winners first, then their 8 value loads issued together (one
   // load per year in sequence would leave each wave waiting out the HBM latency 30 times)
   constexpr int WB = LT_WB;
@@ -192,6 +195,9 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
         const VT vs = (VT)v;
         if constexpr (!EXACT || sizeof(VT) < 8) {
           if (!((double)vs == v)) f32_bad = true;
+        }
+        if constexpr (!std::is_same<VT, int16_t>::value) {
+          if (!(v == __builtin_rint(v) && __builtin_fabs(v) <= 32767.0)) intdata = false;
         }
         L.ys[T][lane] = vs;
         pres |= 1ull << y;
@@ -539,50 +545,65 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
     int xA = 0, xB = 0, xC = 0, xD = 0;
     double yA = 0.0, yB = 0.0, yC = 0.0, yD = 0.0;
     double oA = 0.0, oB = 0.0, oC = 0.0, oD = 0.0;  // oA = OPTa[0] for column 0
-    bool eA = true, eB = true, eC = true, eD = true;  // exactness of the OPTa window slots
+    // tags of the OPTa window slots (lt_pixel.h tag_order; < 256: the value is exact)
+    int gA = 0, gB = 0, gC = 0, gD = 0;
     double SyyAll = 0.0;                // sum of y^2 over the points 0..j
     const bool prune = c >= 0.0;
+    // zero-residual starts of >= 3 points (lt_pixel.h kZero): integer series of int16 range only
+    const bool zok = c > 0.0;
+    const bool zlane = zok && intdata;
     uint64_t amb = 0;
     // column j: wx0 receives point j (its slot held point j-4); wx1..wx3 hold points j-1..j-3;
-    // opt_j..opt_jm3 hold OPTa[j..j-3], and OPTa[j+1] is written over opt_jm3
+    // opt_j..opt_jm3 hold OPTa[j..j-3] (tags tg_*), and OPTa[j+1] is written over opt_jm3
     auto column = [&](const int j, int& wx0, int& wx1, int& wx2, int& wx3, double& wy0,
                       double& wy1, double& wy2, double& wy3, double& opt_j, double& opt_jm1,
-                      double& opt_jm2, double& opt_jm3, bool& ex_j, bool& ex_jm1, bool& ex_jm2,
-                      bool& ex_jm3) __attribute__((always_inline)) {
+                      double& opt_jm2, double& opt_jm3, int& tg_j, int& tg_jm1, int& tg_jm2,
+                      int& tg_jm3) __attribute__((always_inline)) {
       const bool col = j < n;
       double Sy = 0.0, Sxy = 0.0, Syy = 0.0;
       int Sx = 0, Sxx = 0;
-      // interval candidates: smallest upper end (Hi: start i1, value v1) and the two smallest
-      // lower ends (L1 at start iL, L2); Ve/ie: the exact candidates
-      double Ve = inf, Hi = inf, L1 = inf, L2 = inf, v1 = inf;
-      int ie = 0, i1 = 0, iL = -1;
-      // starts in decreasing order ("<=" keeps the smaller start among equal values). First the
-      // 1- and 2-point starts: residual exactly 0, so with an exact OPTa the value is the
-      // reference's own; otherwise an interval of half-width Emax + rounding.
-#pragma unroll
-      for (int s = 0; s <= 1; s++) {
-        const int i = j - s;
-        if (i < 0) continue;  // wave-uniform
-        const double v = c + (s ? opt_jm1 : opt_j);
-        if (s ? ex_jm1 : ex_j) {
+      // interval candidates: smallest upper end (Hi: start i1, value v1, tag n1 of OPTa[j+1] if it
+      // wins) and the two smallest lower ends (L1 at start iL, L2); Ve/ie: the exact candidates;
+      // gv/gi/gt: the best zero-residual start on an inexact OPTa of the group's base (its
+      // interval enters the trackers at the end of the column)
+      double Ve = inf, Hi = inf, L1 = inf, L2 = inf, v1 = inf, gv = inf;
+      int ie = 0, i1 = 0, iL = -1, n1 = -1, gi = -1, gt = 0;
+      auto track = [&](int i, double v, double hi, double lo, int nt) __attribute__((always_inline)) {
+        if (hi <= Hi) {
+          i1 = i;
+          v1 = v;
+          n1 = nt;
+        }
+        Hi = hi <= Hi ? hi : Hi;
+        const bool bl = lo <= L1;
+        L2 = bl ? L1 : (lo < L2 ? lo : L2);
+        L1 = bl ? lo : L1;
+        iL = bl ? i : iL;
+      };
+      // a zero-residual start (worth fl(c + OPTa[i]) in the reference) on OPTa[i] of tag tg
+      // (tg < 0: inexact, tag unknown), in decreasing start order
+      auto zero_start = [&](int i, double v, int tg) __attribute__((always_inline)) {
+        if (tg >= 0 && tg < 256) {  // exact
           if (v <= Ve) {
             Ve = v;
             ie = i;
           }
-        } else {
-          const double w = __builtin_fma(0x1p-50, __builtin_fabs(v), Emax);
-          const double hi = v + w, lo = v - w;
-          if (hi <= Hi) {
-            i1 = i;
-            v1 = v;
-          }
-          Hi = hi <= Hi ? hi : Hi;
-          const bool bl = lo <= L1;
-          L2 = bl ? L1 : (lo < L2 ? lo : L2);
-          L1 = bl ? lo : L1;
-          iL = bl ? i : iL;
+          return;
         }
-      }
+        const double w = __builtin_fma(0x1p-50, __builtin_fabs(v), Emax);
+        const int ord = (!zok || tg < 0) ? 0 : gi < 0 ? 1 : tag_order(tg, gt, v, c);
+        if (ord > 0) {  // the group's new best: the smaller start, value <= the old best
+          gi = i;
+          gt = tg;
+          gv = v;
+        } else if (ord == 0) {
+          track(i, v, v + w, v - w, tg < 0 ? -1 : tg + 1);
+        }  // ord < 0: strictly above the group's best, never the first minimum
+      };
+      // starts in decreasing order ("<=" keeps the smaller start among equal values). First the
+      // 1- and 2-point starts: residual exactly 0
+      zero_start(j, c + opt_j, tg_j);
+      if (j >= 1) zero_start(j - 1, c + opt_jm1, tg_jm1);  // wave-uniform condition
       // prefix bound for the early exit below: every segment ending at j has Syy <= SyyAll
       wx0 = L.xn[j][lane];
       wy0 = (double)L.ys[j][lane];
@@ -597,9 +618,10 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
       // the early-exit bound's screening slack, the same for every start of the column
       const double slack = 4.0 * kScreen * SyyAll * (1.0 + 0x1p-49);
       // start i (>= 3 points) priced from the current sums: value v, its interval [lo, hi] around
-      // the reference value (ex: OPTa[i] is exact), and the early-exit bound for the starts below
-      auto price = [&](int i, double o, bool ex, double& v, double& hi, double& lo,
-                       double& bnd) {
+      // the reference value (tg: tag of OPTa[i]), the early-exit bound for the starts below, and
+      // whether the segment is exactly collinear with a residual that rounds away (zr)
+      auto price = [&](int i, double o, int tg, double& v, double& hi, double& lo, double& bnd,
+                       bool& zr) __attribute__((always_inline)) {
         // closed-form SSE: (m*Syy - Sy^2 - N1^2/D) / m, one reciprocal
         const int m = j - i + 1;  // wave-uniform, >= 3
         const double md = (double)m;
@@ -613,24 +635,29 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
         v = (e + c) + o;  // o = OPTa[i]
         // interval around the reference value: OPT bound + screening bound of this segment +
         // the rounding of this candidate's own two additions
-        const double wopt = ex ? 0.0 : Emax;
-        const double w = __builtin_fma(0x1p-50, __builtin_fabs(v), __builtin_fma(kScreen, Syy, wopt));
+        const double wopt = (tg >= 0 && tg < 256) ? 0.0 : Emax;
+        const double ws = kScreen * Syy;
+        const double w = __builtin_fma(0x1p-50, __builtin_fabs(v), ws + wopt);
         hi = v + w;
         lo = v - w;
         bnd = dp_start_bound_slack(e, o, wopt, c, slack);
-      };
-      // candidates in decreasing start order ("<=" keeps the smaller start among equal values)
-      auto track = [&](int i, double v, double hi, double lo) {
-        if (hi <= Hi) {
-          i1 = i;
-          v1 = v;
+        // the exact-zero test only where the interval reaches a zero residual
+        const bool near0 = zlane && e <= ws;
+        zr = false;
+        if (__ballot(near0)) {
+          if (near0) zr = kZero * Syy < 0x1p-54 * c && sse_exact_zero(t1, D, N1);
         }
-        Hi = hi <= Hi ? hi : Hi;
-        const bool bl = lo <= L1;
-        L2 = bl ? L1 : (lo < L2 ? lo : L2);
-        L1 = bl ? lo : L1;
-        iL = bl ? i : iL;
       };
+      // a start of >= 3 points: a zero-residual start (v recomputed as the reference's
+      // fl(c + OPTa[i])) or an interval candidate that starts a new base if it wins
+      auto offer = [&](int i, double o, int tg, double v, double hi, double lo, bool zr) __attribute__((always_inline)) {
+        if (__ballot(zr)) {
+          if (zr) zero_start(i, c + o, tg);
+        }
+        if (!zr) track(i, v, hi, lo, -1);
+      };
+      // the group's upper end (for the early exit; inf while the group is empty)
+      auto group_hi = [&]() __attribute__((always_inline)) { return gv + __builtin_fma(0x1p-50, __builtin_fabs(gv), Emax); };
       // the 1- and 2-point starts (priced above) only add their points to the sums
       add_xy(wx0, wy0);
       if (j >= 1) add_xy(wx1, wy1);
@@ -642,16 +669,19 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
       if (more) {  // starts j-2 and j-3 from the register window
         const bool two = j >= 3;
         double va, ha, la, ba, vb = 0.0, hb = 0.0, lb = 0.0, bb = 0.0;
+        bool za, zb = false;
         add_xy(wx2, wy2);
-        price(j - 2, opt_jm2, ex_jm2, va, ha, la, ba);
+        price(j - 2, opt_jm2, tg_jm2, va, ha, la, ba, za);
         if (two) {
           add_xy(wx3, wy3);
-          price(j - 3, opt_jm3, ex_jm3, vb, hb, lb, bb);
+          price(j - 3, opt_jm3, tg_jm3, vb, hb, lb, bb, zb);
         }
-        track(j - 2, va, ha, la);
-        if (two) track(j - 3, vb, hb, lb);
+        offer(j - 2, opt_jm2, tg_jm2, va, ha, la, za);
+        if (two) offer(j - 3, opt_jm3, tg_jm3, vb, hb, lb, zb);
         if (prune) {
-          const double Hb = Hi < Ve ? Hi : Ve;
+          double Hb = Hi < Ve ? Hi : Ve;
+          const double gh = group_hi();
+          Hb = gh < Hb ? gh : Hb;
           if (!__ballot(col && !(ba > Hb || (two && bb > Hb)))) more = false;
         }
         more = more && two;
@@ -661,56 +691,71 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
         const bool two = i >= 1;                            // wave-uniform
         add_xy(L.xn[i][lane], (double)L.ys[i][lane]);
         double va, ha, la, ba, vb = 0.0, hb = 0.0, lb = 0.0, bb = 0.0;
-        price(i, OPTa[i], (exact >> i) & 1, va, ha, la, ba);
+        bool za, zb = false;
+        const double oa = OPTa[i];
+        const int ta = ((exact >> i) & 1) ? 0 : -1;  // tags are kept in the window only
+        price(i, oa, ta, va, ha, la, ba, za);
+        double ob = 0.0;
+        int tb = 0;
         if (two) {
           add_xy(L.xn[i - 1][lane], (double)L.ys[i - 1][lane]);
-          price(i - 1, OPTa[i - 1], (exact >> (i - 1)) & 1, vb, hb, lb, bb);
+          ob = OPTa[i - 1];
+          tb = ((exact >> (i - 1)) & 1) ? 0 : -1;
+          price(i - 1, ob, tb, vb, hb, lb, bb, zb);
         }
-        track(i, va, ha, la);
-        if (two) track(i - 1, vb, hb, lb);
+        offer(i, oa, ta, va, ha, la, za);
+        if (two) offer(i - 1, ob, tb, vb, hb, lb, zb);
         if (prune) {
-          const double Hb = Hi < Ve ? Hi : Ve;
+          double Hb = Hi < Ve ? Hi : Ve;
+          const double gh = group_hi();
+          Hb = gh < Hb ? gh : Hb;
           if (!__ballot(col && !(ba > Hb || (two && bb > Hb)))) break;
         }
       }
+      if (gi >= 0) {  // the group's best enters the trackers
+        const double w = __builtin_fma(0x1p-50, __builtin_fabs(gv), Emax);
+        track(gi, gv, gv + w, gv - w, gt + 1);
+      }
       const double H = Hi < Ve ? Hi : Ve;  // the exact minimum lies in [min(L1, Ve), H]
-      int a;
+      int a, tnew;
       double vnew, enew = 0.0;
-      bool exnew = false;
       if (L1 > H) {  // no inexact interval reaches H: the exact candidates decide
         a = ie;
         vnew = Ve;
-        exnew = true;
+        tnew = 0;
       } else if (iL == i1 && L2 > H && Ve > H) {  // one candidate lies below all others
         a = i1;
         vnew = v1;
+        // a zero-residual winner adds c to its OPTa's tag; any other starts a new base
+        tnew = n1 >= 0 ? n1 : (j + 1) << 8;
         // its half-width, rounded up: Hi = fl(v1 + w1) >= v1 + w1 - ulp(Hi) / 2
         enew = __builtin_fma(Hi - v1, 1.0 + 0x1p-50, 0x1p-50 * __builtin_fabs(Hi));
       } else {
         if (col) amb |= 1ull << j;
         a = v1 <= Ve ? i1 : ie;
         vnew = v1 <= Ve ? v1 : Ve;
+        tnew = (j + 1) << 8;
         const double Lo = L1 < Ve ? L1 : Ve;
         enew = (H - Lo) * (1.0 + 0x1p-40) + 0x1p-50 * __builtin_fabs(vnew);
       }
       if (col) {
         ag_set(j, a);
         OPTa[j + 1] = vnew;  // wave-uniform index
-        if (exnew) exact |= 2ull << j;
+        if (tnew < 256) exact |= 2ull << j;
         Emax = enew > Emax ? enew : Emax;
         opt_jm3 = vnew;  // OPTa[j+1]: the slot of OPTa[j-3], which no later column reads
-        ex_jm3 = exnew;
+        tg_jm3 = tnew;
       }
     };
     for (int jj = 0; jj < nmax; jj += 4) {
       const int j = __builtin_amdgcn_readfirstlane(jj);  // column index in an SGPR
-      column(j, xA, xB, xC, xD, yA, yB, yC, yD, oA, oB, oC, oD, eA, eB, eC, eD);
+      column(j, xA, xB, xC, xD, yA, yB, yC, yD, oA, oB, oC, oD, gA, gB, gC, gD);
       if (j + 1 < nmax)
-        column(j + 1, xD, xA, xB, xC, yD, yA, yB, yC, oD, oA, oB, oC, eD, eA, eB, eC);
+        column(j + 1, xD, xA, xB, xC, yD, yA, yB, yC, oD, oA, oB, oC, gD, gA, gB, gC);
       if (j + 2 < nmax)
-        column(j + 2, xC, xD, xA, xB, yC, yD, yA, yB, oC, oD, oA, oB, eC, eD, eA, eB);
+        column(j + 2, xC, xD, xA, xB, yC, yD, yA, yB, oC, oD, oA, oB, gC, gD, gA, gB);
       if (j + 3 < nmax)
-        column(j + 3, xB, xC, xD, xA, yB, yC, yD, yA, oB, oC, oD, oA, eB, eC, eD, eA);
+        column(j + 3, xB, xC, xD, xA, yB, yC, yD, yA, oB, oC, oD, oA, gB, gC, gD, gA);
     }
     // find_segments (utils.py:633-644): starts of the optimal segments + the last point
     if (n >= 1) {

@@ -54,7 +54,7 @@ struct RuleState1 {
   int32_t on = LT_NODATA, du = LT_NODATA;
   double mag = (double)LT_NODATA, init = (double)LT_NODATA;
 
-  __host__ __device__ void offer(const lt_rule& R, int pre_mode, int32_t d_on, int32_t d_du,
+  __host__ __device__ __attribute__((always_inline)) void offer(const lt_rule& R, int pre_mode, int32_t d_on, int32_t d_du,
                                  double d_init, double d_mag, int& status) {
     bool match = true;
     if (R.onset_op == LT_Q_EQ) match = match && ((double)d_on == R.onset_val);
@@ -83,7 +83,7 @@ struct RuleState1 {
     }
   }
 
-  __host__ __device__ void write(const lt_rule& R, const lt_tile_out& out, int64_t q) const {
+  __host__ __device__ __attribute__((always_inline)) void write(const lt_rule& R, const lt_tile_out& out, int64_t q) const {
     if (out.matched) out.matched[q] = have ? 1 : 0;
     if (out.class_val) out.class_val[q] = have ? R.class_val : LT_NODATA;
     if (out.onset_year) out.onset_year[q] = on;
@@ -200,6 +200,35 @@ __host__ __device__ inline double dp_start_bound(double e, double opta, double e
   return dp_start_bound_slack(e, opta, eopt, c, 4.0 * kScreen * SyyAll * (1.0 + 0x1p-49));
 }
 
+// Zero-residual starts. The reference prices start i of column j as fl(fl(e + c) + OPT[i])
+// (utils.py:627) with e = 0.0 exactly for 1-2 points (no residuals, utils.py:592-597) and e >= 0
+// the emulated dgelsd residual otherwise. When the segment's exact SSE is 0 (collinear points)
+// and kZero * Syy < 2^-54 c, e lies below half an ulp of c, so fl(e + c) = c: the start is worth
+// fl(c + OPT[i]) like a 1-2 point start, and is exact whenever OPT[i] is.
+// kZero bounds the emulated residual of exactly collinear segments: tests/test_screening.py
+// measures at most 2^-93 Syy (m <= 64, int16 values, gapped x sets).
+constexpr double kZero = 0x1p-80;
+
+// t1 * D == N1^2 exactly (the closed form's numerator m*D*SSE is 0): t1, D and N1 are exact
+// integers in binary64 when the values are integers of int16 range (|Sy| < 2^21, Syy < 2^36),
+// and each product is split exactly into a double pair.
+__host__ __device__ inline bool sse_exact_zero(double t1, double D, double N1) {
+  const double p = t1 * D, q = N1 * N1;
+  return p == q && __builtin_fma(t1, D, -p) == __builtin_fma(N1, N1, -q);
+}
+
+// Tags of inexact OPT values. tag = (b << 8) | t says OPT[k] = g^t(OPT[b]) with g(x) = fl(c + x)
+// and b >= 1 (tag < 256: OPT[k] is exact). Two zero-residual starts whose OPT values share a
+// base are ordered without knowing OPT[b]: g is non-decreasing for c >= 0, so t <= t' gives
+// fl(c + OPT) <= fl(c + OPT'), and strictly increasing while c exceeds the rounding of x + c.
+// Returns whether a start of tag `tn` (a smaller start than the one of tag `tg`) is provably
+// <= (1), provably > (-1), or neither (0) in value.
+__host__ __device__ inline int tag_order(int tn, int tg, double v, double c) {
+  if ((tn >> 8) != (tg >> 8)) return 0;
+  if ((tn & 255) <= (tg & 255)) return 1;
+  return c > 0x1p-50 * __builtin_fabs(v) ? -1 : 0;
+}
+
 // segmented_least_squares' DP (utils.py:618-631) with candidate screening.
 // For column j every start i is first priced with the closed-form SSE of its segment (exact
 // integer sums for integer data); only the starts whose price lies within the error window of
@@ -283,21 +312,49 @@ template <int MAXY>
 __host__ __device__ inline bool dp_lazy(int n, const uint8_t* xs, const double* ys, double c,
                                         uint8_t* arg, uint64_t* amb_out = nullptr) {
   double OPTa[MAXY + 1], E[MAXY + 1];
+  int TG[MAXY + 1];  // tags (tag_order) of the OPT values
   uint64_t amb = 0;
   OPTa[0] = 0.0;
   E[0] = 0.0;
+  TG[0] = 0;
+  // integer values of int16 range: the closed form's sums are exact (sse_exact_zero)
+  bool intdata = true;
+  for (int k = 0; k < n; k++)
+    intdata = intdata && ys[k] == (double)(int)ys[k] && ys[k] >= -32768.0 && ys[k] <= 32767.0;
+  const bool zero_ok = c > 0.0;
   double SyyAll = 0.0;  // sum of y^2 over the points 0..j (early exit, as in dp_screened)
   for (int j = 0; j < n; j++) {
     SyyAll += ys[j] * ys[j];
     double Sy = 0.0, Sxy = 0.0, Syy = 0.0;
     int Sx = 0, Sxx = 0;
-    // Exact candidates (1-2 point segment: residual exactly 0, on an exact OPT) are computed
-    // with the reference's own operations, so their value IS the reference's; the others carry
-    // an interval [v - w, v + w] around the reference value.
+    // Exact candidates (zero-residual start on an exact OPT) are computed with the reference's
+    // own operations, so their value IS the reference's; the others carry an interval
+    // [v - w, v + w] around the reference value. Zero-residual starts on inexact OPT values of
+    // one base form a group whose best member is known exactly (tag_order); only that member
+    // enters the interval trackers, at the end of the column.
     const double inf = __builtin_inf();
     double Ve = inf;                   // min exact value; ie = first start attaining it
     double Hi = inf, Li1 = inf, Li2 = inf, vHi = 0.0, wHi = 0.0, vbest = inf;
-    int ie = -1, iHi = -1, ibest = -1, iL1 = -2;
+    int ie = -1, iHi = -1, ibest = -1, iL1 = -2, tHi = -1;
+    double gv = 0.0, gw = 0.0;
+    int gi = -1, gtag = 0;
+    auto track = [&](int i, double v, double w, int ntag) {
+      const double lo = v - w, hi = v + w;
+      if (hi <= Hi) {
+        Hi = hi;
+        iHi = i;
+        vHi = v;
+        wHi = w;
+        tHi = ntag;
+      }
+      if (lo <= Li1) {  // the two smallest lower ends (equal ones count twice)
+        Li2 = Li1;
+        Li1 = lo;
+        iL1 = i;
+      } else if (lo < Li2) {
+        Li2 = lo;
+      }
+    };
     for (int i = j; i >= 0; i--) {
       const int xi = xs[i];
       const double yi = ys[i];
@@ -307,7 +364,8 @@ __host__ __device__ inline bool dp_lazy(int n, const uint8_t* xs, const double* 
       Sxy += (double)xi * yi;
       Syy += yi * yi;
       const int m = j - i + 1;
-      double e = 0.0, w = E[i];
+      double e = 0.0, ws = 0.0;
+      bool zr = m <= 2;
       if (m >= 3) {
         const double md = (double)m;
         const double D = (double)(m * Sxx - Sx * Sx);
@@ -315,48 +373,60 @@ __host__ __device__ inline bool dp_lazy(int n, const uint8_t* xs, const double* 
         const double N1 = md * Sxy - (double)Sx * Sy;
         e = (t1 - N1 * N1 / D) / md;
         if (e < 0.0) e = 0.0;
-        w += kScreen * Syy;
+        ws = kScreen * Syy;
+        if (zero_ok && intdata && e <= ws && kZero * Syy < 0x1p-54 * c &&
+            sse_exact_zero(t1, D, N1)) {
+          zr = true;
+          e = 0.0;
+          ws = 0.0;
+        }
       }
       const double v = (e + c) + OPTa[i];
-      if (v <= vbest) {  // i descends: "<=" keeps the smaller start on equal values
-        vbest = v;
-        ibest = i;
-      }
-      if (w == 0.0) {
+      bool tracked = true;
+      if (zr && E[i] == 0.0) {
         if (v <= Ve) {
           Ve = v;
           ie = i;
         }
-        continue;
+      } else if (zr && zero_ok) {
+        const double w = E[i] + 0x1p-50 * __builtin_fabs(v);
+        const int ord = gi < 0 ? 1 : tag_order(TG[i], gtag, v, c);
+        if (ord > 0) {  // the group's new best (i descends: the smaller start, value <=)
+          gi = i;
+          gtag = TG[i];
+          gv = v;
+          gw = w;
+        } else if (ord < 0) {
+          tracked = false;  // strictly above the group's best: never the first minimum
+        } else {
+          track(i, v, w, TG[i] + 1);
+        }
+      } else {
+        track(i, v, E[i] + ws + 0x1p-50 * __builtin_fabs(v), -1);
       }
-      w += 0x1p-50 * __builtin_fabs(v);
-      const double lo = v - w, hi = v + w;
-      if (hi <= Hi) {
-        Hi = hi;
-        iHi = i;
-        vHi = v;
-        wHi = w;
+      if (tracked && v <= vbest) {  // i descends: "<=" keeps the smaller start on equal values
+        vbest = v;
+        ibest = i;
       }
-      if (lo <= Li1) {  // the two smallest lower ends (equal ones count twice)
-        Li2 = Li1;
-        Li1 = lo;
-        iL1 = i;
-      } else if (lo < Li2) {
-        Li2 = lo;
-      }
-      const double Hc = Hi < Ve ? Hi : Ve;
+      double Hc = Hi < Ve ? Hi : Ve;
+      if (gi >= 0 && gv + gw < Hc) Hc = gv + gw;
       if (m >= 3 && c >= 0.0 && dp_start_bound(e, OPTa[i], E[i], c, SyyAll) > Hc) break;
     }
+    if (gi >= 0) track(gi, gv, gw, gtag + 1);
     const double H = Hi < Ve ? Hi : Ve;  // the exact minimum lies in [min lower bound, H]
     if (Li1 > H) {  // no interval reaches H: the exact candidates decide, bit-exactly
       arg[j] = (uint8_t)ie;
       OPTa[j + 1] = Ve;
       E[j + 1] = 0.0;
+      TG[j + 1] = 0;
     } else if (iL1 == iHi && Li2 > H && Ve > H) {  // one start lies below all others
       arg[j] = (uint8_t)iHi;
       OPTa[j + 1] = vHi;
       E[j + 1] = wHi;
+      // a zero-residual start adds c to its OPT value's tag; any other starts a new base
+      TG[j + 1] = tHi >= 0 ? tHi : (j + 1) << 8;
     } else {
+      TG[j + 1] = (j + 1) << 8;
       amb |= 1ull << j;
       arg[j] = (uint8_t)ibest;
       OPTa[j + 1] = vbest;

@@ -58,6 +58,16 @@ extern "C" uint64_t ltx_dp_lazy(int n, const uint8_t* xs, const double* ys, doub
   return amb;
 }
 
+// The exact-OPT DP (dp_screened: LAPACK-emulated residual for every start in the window) on one
+// compacted series: the argmin of every column.
+extern "C" int ltx_dp_exact(int n, const uint8_t* xs, const double* ys, double c, uint8_t* arg) {
+  double OPT[65];
+  OPT[0] = 0.0;
+  int status = 0;
+  lt::dp_screened<64>(n, xs, ys, c, OPT, arg, status);
+  return status;
+}
+
 // The integer-x fused variant (lstsq_xint) on integer x given as doubles.
 extern "C" int ltx_lstsq_xint(int m, const double* x, const double* y, int need_solution,
                               int need_ssr, double* out3) {

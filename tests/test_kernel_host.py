@@ -70,3 +70,64 @@ def test_kernel_code_on_host_matches_oracle_synthetic(hc):
             same = ((a.view(np.int64) == b.view(np.int64)) | (np.isnan(a) & np.isnan(b))
                     if a.dtype.kind == 'f' else a == b)
             assert same.all(), (seed, f, int((~same).sum()))
+
+
+def _vertices(arg, n):
+    v, j = {n - 1}, n - 1
+    while j >= 0:
+        v.add(int(arg[j]))
+        j = int(arg[j]) - 1
+    return sorted(v)
+
+
+def _tie_heavy_series(rng, n):
+    """Small-integer series built from collinear runs (zero-residual segments of >= 3 points,
+    lt_pixel.h kZero), flat stretches and unit noise: the DP's ties and exact-zero starts."""
+    kind = rng.integers(0, 4)
+    if kind == 0:
+        ys = rng.integers(0, 4, n)
+    elif kind == 1:  # piecewise-linear integer runs
+        ys, v = [], int(rng.integers(-50, 50))
+        while len(ys) < n:
+            slope, run = int(rng.integers(-5, 6)), int(rng.integers(2, 7))
+            for _ in range(run):
+                ys.append(v)
+                v += slope
+        ys = np.array(ys[:n])
+    elif kind == 2:  # runs plus occasional unit noise
+        ys = np.cumsum(rng.integers(-2, 3, n)) + (rng.random(n) < 0.2) * rng.integers(-1, 2, n)
+    else:  # synthetic-like magnitudes
+        ys = 1200 + np.round(rng.normal(0, 40, n)) - 10 * np.arange(n)
+    xs = np.arange(n) if rng.integers(0, 3) else np.sort(rng.choice(64, n, replace=False))
+    return np.ascontiguousarray(xs, np.uint8), np.ascontiguousarray(ys, np.float64)
+
+
+def test_lazy_dp_with_zero_residual_groups_matches_exact_dp(hc):
+    """lt_pixel.h dp_lazy (closed-form intervals, exact-zero starts, same-base tag order) never
+    decides a column differently from the exact-OPT DP on the path it reports as decided."""
+    u8p = ctypes.POINTER(ctypes.c_uint8)
+    f64p = ctypes.POINTER(ctypes.c_double)
+    hc.ltx_dp_lazy.argtypes = [ctypes.c_int, u8p, f64p, ctypes.c_double, u8p,
+                               ctypes.POINTER(ctypes.c_int)]
+    hc.ltx_dp_lazy.restype = ctypes.c_uint64
+    hc.ltx_dp_exact.argtypes = [ctypes.c_int, u8p, f64p, ctypes.c_double, u8p]
+    rng = np.random.default_rng(21)
+    n_dec = n_def = 0
+    for _ in range(6000):
+        n = int(rng.integers(3, 49))
+        xs, ys = _tie_heavy_series(rng, n)
+        c = float(rng.choice([1.0, 0.5, 10.0, 3.0, 1e-4, 2.0 / 3.0]))
+        a1 = np.zeros(64, np.uint8)
+        a2 = np.zeros(64, np.uint8)
+        d = ctypes.c_int(0)
+        hc.ltx_dp_lazy(n, xs.ctypes.data_as(u8p), ys.ctypes.data_as(f64p), c,
+                       a1.ctypes.data_as(u8p), ctypes.byref(d))
+        hc.ltx_dp_exact(n, xs.ctypes.data_as(u8p), ys.ctypes.data_as(f64p), c,
+                        a2.ctypes.data_as(u8p))
+        if d.value:
+            n_def += 1
+            continue
+        n_dec += 1
+        assert _vertices(a1, n) == _vertices(a2, n), (list(xs), list(ys), c)
+    print('lazy DP decided %d series, deferred %d' % (n_dec, n_def))
+    assert n_dec > 4000

@@ -139,3 +139,82 @@ def test_closed_form_restatement_is_exact_on_small_integers(m):
     exact, _ = exact_sse(x, y)
     cf = closed_form(x, y)
     assert abs(F(cf) - exact) <= abs(exact) * F(2) ** -50 + F(2) ** -60
+
+
+K_ZERO = 2.0 ** -80  # lt_pixel.h kZero
+
+
+def collinear_segments(seed, count):
+    """Exactly collinear integer segments of int16 range: y = a + b*(x - x0) with integer a, b,
+    consecutive and gapped x sets, m from 3 to 64."""
+    rng = np.random.default_rng(seed)
+    out = []
+    while len(out) < count:
+        m = int(rng.choice([3, 3, 3, 4, 4, 5, 6, 8, 12, 20, 40, 64]))
+        if rng.integers(0, 2):
+            x0 = int(rng.integers(0, 64 - m + 1))
+            x = np.arange(x0, x0 + m)
+        else:
+            x = np.sort(rng.choice(64, m, replace=False))
+        b = int(rng.integers(-2000, 2001)) if rng.integers(0, 2) else int(rng.integers(-3, 4))
+        a = int(rng.integers(-32768, 32768))
+        y = a + b * (x - x[0])
+        if y.min() < -32768 or y.max() > 32767:
+            continue
+        out.append(([int(v) for v in x], [float(v) for v in y]))
+    return out
+
+
+def test_collinear_residual_bound():
+    """kZero: on an exactly collinear segment the reference's residual (the emulated dgelsd,
+    bit-exact with numpy's) is pure rounding noise, quadratic in the unit roundoff. The kernel
+    treats such a start as worth fl(c + OPT) when kZero * Syy < 2^-54 * c, so kZero must bound it;
+    require a 2^10 margin."""
+    worst = 0.0
+    n = 0
+    for x, y in collinear_segments(11, 4000):
+        rc, slope, icpt, ssr = oracle.lstsq(np.array(x, float), np.array(y, float))
+        assert rc == 0
+        syy = sum(v * v for v in y)
+        if syy == 0:
+            continue
+        worst = max(worst, ssr / syy)
+        n += 1
+        assert ssr <= K_ZERO * MARGIN * syy, (x, y, ssr)
+    print('collinear segments %d: residual/Syy <= 2^%.1f (kZero 2^-80)' % (
+        n, math.log2(worst or 2.0 ** -200)))
+
+
+def sse_exact_zero(x, y):
+    """lt_pixel.h sse_exact_zero on the closed form's sums as lt_fast.h price() forms them."""
+    Sx = Sxx = 0
+    Sy = Sxy = Syy = 0.0
+    for xi, yi in zip(reversed(x), reversed(y)):
+        Sx += xi
+        Sxx += xi * xi
+        Sy = Sy + yi
+        Sxy = fma(float(xi), yi, Sxy)
+        Syy = fma(yi, yi, Syy)
+    m = len(x)
+    md = float(m)
+    D = float(m * Sxx - Sx * Sx)
+    t1 = fma(md, Syy, -(Sy * Sy))
+    N1 = fma(md, Sxy, -(float(Sx) * Sy))
+    p, q = t1 * D, N1 * N1
+    return p == q and fma(t1, D, -p) == fma(N1, N1, -q)
+
+
+def test_exact_zero_test_is_exact_on_int16_segments():
+    """sse_exact_zero says 'collinear' exactly when the exact rational SSE is 0, for integer
+    values of int16 range (where every sum it uses is an exact binary64 integer)."""
+    rng = np.random.default_rng(3)
+    segs = collinear_segments(12, 600)
+    # near misses: one value off by one (the smallest nonzero SSE an integer series can have)
+    for x, y in collinear_segments(13, 600):
+        k = int(rng.integers(0, len(y)))
+        y = list(y)
+        y[k] += 1.0 if y[k] < 32767 else -1.0
+        segs.append((x, y))
+    for x, y in segs:
+        exact, _ = exact_sse(x, y)
+        assert sse_exact_zero(x, y) == (exact == 0), (x, y, exact)
