@@ -229,6 +229,9 @@ def main():
                     help='end-to-end steps (H2D bands, D2H outputs) after the timed ones; 0: none')
     ap.add_argument('--group', type=int, default=0,
                     help='tiles per lt_analyze_tiles call (0: all of a scene, or 1 when gathering)')
+    ap.add_argument('--no-trendline', action='store_true',
+                    help='attribution runs only: leave out the per-year trendline planes of a '
+                         'trendline config (c5)')
     ap.add_argument('--serial-load', action='store_true',
                     help='run the index_eqn kernels on the analyze stream (no load stream)')
     args = ap.parse_args()
@@ -248,7 +251,10 @@ def main():
             dist.init_process_group('nccl', device_id=torch.device('cuda', local))
         else:
             dist.init_process_group(backend)
-    cfg = CONFIGS[args.config]
+    cfg = dict(CONFIGS[args.config])
+    if args.no_trendline:
+        cfg['trendline'] = False
+        cfg['desc'] += ' (attribution run: trendline planes left out)'
     P = args.pixels or cfg['pixels']
     dev = torch.device('cuda', local)
     mosaic_cfg = 'scenes' in cfg

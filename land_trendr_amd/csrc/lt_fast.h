@@ -203,15 +203,8 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
         pres |= 1ull << y;
         T++;
         if (out.val_raw) out.val_raw[q] = v;
-      } else {
-        if (out.val_raw) out.val_raw[q] = nan;
-        if (out.val_fit) out.val_fit[q] = nan;
-        if (out.fit_m) out.fit_m[q] = nan;
-        if (out.fit_b) out.fit_b[q] = nan;
-        if (out.right_m) out.right_m[q] = nan;
-        if (out.right_b) out.right_b[q] = nan;
-        if (out.spike) out.spike[q] = 0;
-        if (out.vertex) out.vertex[q] = 0;
+      } else if (out.val_raw) {  // the other per-year planes: the year-major output loop
+        out.val_raw[q] = nan;
       }
     }
   }
@@ -773,47 +766,125 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
   // deferred lanes stay in the wave (the loops below use wave collectives) but do nothing more
   if (deferred) vmask = 0;
 
-  // ---- vertices2eqns + eqns2fitted_points in lockstep over the vertex number q ----
-  // per-year planes requested (launch-uniform): otherwise the walk over the points is skipped
+  // ---- vertices2eqns + eqns2fitted_points (utils.py:646-722) ----
+  // per-year planes requested (launch-uniform)
   const bool year_out = out.val_fit || out.fit_m || out.fit_b || out.right_m || out.right_b ||
                         out.spike || out.vertex;
-  const int nv = __builtin_popcountll(vmask);
-  const int nvmax = wave_max(nv);
-  uint64_t vrem = vmask;  // vertices from q on: vertex q is its lowest bit
-  double pm = 0.0, pb = 0.0;   // eqn of vertex q-1
   RuleState1 rs[RMAX];
   double prev_fit = 0.0;
   int32_t prev_year = 0;
-  int ta = 0;                  // present index of vertex q (vertex 0 is the first point)
-  uint64_t wrem = pres;        // year slots of the present points from ta on
-  for (int q = 0; q < nvmax; q++) {
-    const bool act = q < nv;
-    const int ka = act ? __builtin_ctzll(vrem) : 0;
-    if (act) vrem &= vrem - 1;
-    const bool has_next = act && q + 1 < nv;
-    const int kb = has_next ? __builtin_ctzll(vrem) : ka;
-    double cm = pm, cb = pb;
-    // one LAPACK-emulated fit per vertex number for the whole wave (lanes without a next
-    // vertex reuse the previous equation, utils.py:662)
-    const int mseg = has_next ? kb - ka + 1 : 2;
-    const int kbase = has_next ? ka : 0;
-    double sm = 0.0, sbv = 0.0;
-    if (__ballot(has_next)) {
-      const int rc = lsq_fit_lockstep(
-          has_next, mseg, [&](int k) { return (int)L.xn[kbase + k][lane]; },
-          [&](int k) { return (double)L.ys[kbase + k][lane]; }, xtab, sm, sbv);
-      if (has_next) {
-        if (rc < 0) status |= LT_ST_NUMERIC;
-        cm = sm;
-        cb = sbv;
+  // parse_disturbances / match_rule (classes.py:156-232): the segment ending at vertex q > 0
+  auto offer_rules = [&](int q, int32_t yr, double fit_vertex) __attribute__((always_inline)) {
+    if (q > 0) {
+#pragma unroll
+      for (int r = 0; r < RMAX; r++)
+        if (r < P.n_rules)
+          rs[r].offer(P.rules[r], P.pre_threshold_mode, prev_year, yr - prev_year, prev_fit,
+                      prev_fit - fit_vertex, status);
+    }
+    prev_fit = fit_vertex;
+    prev_year = yr;
+  };
+  if (year_out) {
+    // Year-major: every year slot is one wave-uniform step and each per-year plane is written
+    // one coalesced row at a time (lane l -> pixel p, all lanes the same year). A lane reaching
+    // a vertex that has a next vertex needs that segment's fit: one LAPACK-emulated fit per year
+    // for the lanes that need it (lanes without a next vertex reuse the previous equation,
+    // utils.py:662). Deferred and dead lanes write nothing (the resolve stage writes them).
+    const bool emit = live && !deferred;
+    const bool good = emit && ok;
+    uint64_t vrem = vmask;           // vertices not reached yet (non-spike indices)
+    double pm = 0.0, pb = 0.0;       // eqn of the previous vertex
+    double cm = 0.0, cb = 0.0;       // eqn of the current vertex (right eqn of the points)
+    int t = 0, k = 0, q = 0;         // present index, non-spike index, vertex number
+    for (int y = 0; y < Y; y++) {    // wave-uniform
+      const bool pr = good && ((pres >> y) & 1);
+      const bool sp = pr && ((spike >> t) & 1);
+      const bool isv = pr && !sp && ((vrem >> k) & 1);
+      const uint64_t after = vrem & (vrem - 1);  // vertices after this one
+      const bool nextfit = isv && after != 0;
+      if (__ballot(nextfit)) {
+        const int kb = nextfit ? __builtin_ctzll(after) : k + 1;
+        const int kbase = nextfit ? k : 0;
+        double sm = 0.0, sbv = 0.0;
+        const int rc = lsq_fit_lockstep(
+            nextfit, kb - kbase + 1, [&](int i) { return (int)L.xn[kbase + i][lane]; },
+            [&](int i) { return (double)L.ys[kbase + i][lane]; }, xtab, sm, sbv);
+        if (nextfit) {
+          if (rc < 0) status |= LT_ST_NUMERIC;
+          pm = cm;
+          pb = cb;
+          cm = sm;
+          cb = sbv;
+        }
+      }
+      if (isv && !nextfit) {  // the last vertex: left eqn = right eqn = the previous one
+        pm = cm;
+        pb = cb;
+      }
+      const double x = (double)(L.year[y] - y0);
+      double fv = (cm * x) + cb, fmv = cm, fbv = cb;
+      if (isv && q > 0 && !(pm == cm && pb == cb)) {
+        const double raw_v = (double)L.ys[k][lane];
+        const double fl = (pm * x) + pb;
+        if (__builtin_fabs(fl - raw_v) <= __builtin_fabs(fv - raw_v)) {
+          fv = fl;
+          fmv = pm;
+          fbv = pb;
+        }
+      }
+      if (isv) {
+        offer_rules(q, L.year[y], fv);
+        vrem = after;
+        q++;
+      }
+      if (emit) {  // absent years and pixels the reference raises for: NaN / 0
+        const int64_t o = (int64_t)y * os + p;
+        if (out.val_fit) out.val_fit[o] = pr ? fv : nan;
+        if (out.fit_m) out.fit_m[o] = pr ? fmv : nan;
+        if (out.fit_b) out.fit_b[o] = pr ? fbv : nan;
+        if (out.right_m) out.right_m[o] = pr ? cm : nan;
+        if (out.right_b) out.right_b[o] = pr ? cb : nan;
+        if (out.spike) out.spike[o] = sp ? 1 : 0;
+        if (out.vertex) out.vertex[o] = isv ? 1 : 0;
+      }
+      if (pr) {
+        if (!sp) k++;
+        t++;
       }
     }
-    // emit the vertex point and the points up to the next vertex (spikes included): walk the
-    // present points from the vertex, counting non-spike ones until the next vertex
-    const double raw_v = act ? (double)L.ys[ka][lane] : 0.0;
-    double fit_vertex = 0.0;
-    if (!year_out) {  // labels only: the fitted value at the vertex is all the rules need
+  } else {
+    // labels only, in lockstep over the vertex number q: the fitted value at each vertex is all
+    // the rules need
+    const int nv = __builtin_popcountll(vmask);
+    const int nvmax = wave_max(nv);
+    uint64_t vrem = vmask;  // vertices from q on: vertex q is its lowest bit
+    double pm = 0.0, pb = 0.0;   // eqn of vertex q-1
+    for (int q = 0; q < nvmax; q++) {
+      const bool act = q < nv;
+      const int ka = act ? __builtin_ctzll(vrem) : 0;
+      if (act) vrem &= vrem - 1;
+      const bool has_next = act && q + 1 < nv;
+      const int kb = has_next ? __builtin_ctzll(vrem) : ka;
+      double cm = pm, cb = pb;
+      // one LAPACK-emulated fit per vertex number for the whole wave (lanes without a next
+      // vertex reuse the previous equation, utils.py:662)
+      const int mseg = has_next ? kb - ka + 1 : 2;
+      const int kbase = has_next ? ka : 0;
+      double sm = 0.0, sbv = 0.0;
+      if (__ballot(has_next)) {
+        const int rc = lsq_fit_lockstep(
+            has_next, mseg, [&](int k) { return (int)L.xn[kbase + k][lane]; },
+            [&](int k) { return (double)L.ys[kbase + k][lane]; }, xtab, sm, sbv);
+        if (has_next) {
+          if (rc < 0) status |= LT_ST_NUMERIC;
+          cm = sm;
+          cb = sbv;
+        }
+      }
+      const double raw_v = act ? (double)L.ys[ka][lane] : 0.0;
       const double x = act ? (double)L.xn[ka][lane] : 0.0;  // the vertex's year offset
+      double fit_vertex;
       if (q > 0 && !(pm == cm && pb == cb)) {
         const double fl = (pm * x) + pb;
         const double fr = (cm * x) + cb;
@@ -821,62 +892,10 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
       } else {
         fit_vertex = (cm * x) + cb;
       }
+      if (act) offer_rules(q, y0 + L.xn[ka][lane], fit_vertex);
+      pm = cm;
+      pb = cb;
     }
-    int t = ta, kk = ka;
-    bool going = act && year_out;
-    for (int s = 0; __ballot(going); s++) {
-      if (!going) continue;
-      if (s > 0) {
-        const bool nonspike = t >= 64 || !((spike >> t) & 1);
-        if (!has_next || (nonspike && ++kk == kb)) {  // the next vertex, or the last one done
-          going = false;
-          ta = t;
-          continue;
-        }
-      }
-      const int y = __builtin_ctzll(wrem);
-      wrem &= wrem - 1;
-      const double x = (double)(L.year[y] - y0);
-      double fv, fmv, fbv;
-      if (s == 0 && q > 0 && !(pm == cm && pb == cb)) {
-        const double fl = (pm * x) + pb;
-        const double fr = (cm * x) + cb;
-        if (__builtin_fabs(fl - raw_v) <= __builtin_fabs(fr - raw_v)) {
-          fv = fl; fmv = pm; fbv = pb;
-        } else {
-          fv = fr; fmv = cm; fbv = cb;
-        }
-      } else {
-        fv = (cm * x) + cb;
-        fmv = cm;
-        fbv = cb;
-      }
-      if (s == 0) fit_vertex = fv;
-      const int64_t o = (int64_t)y * os + p;
-      if (out.val_fit) out.val_fit[o] = fv;
-      if (out.fit_m) out.fit_m[o] = fmv;
-      if (out.fit_b) out.fit_b[o] = fbv;
-      if (out.right_m) out.right_m[o] = cm;
-      if (out.right_b) out.right_b[o] = cb;
-      if (out.spike) out.spike[o] = (uint8_t)((spike >> t) & 1);
-      if (out.vertex) out.vertex[o] = s == 0 ? 1 : 0;
-      t++;
-    }
-    // parse_disturbances / match_rule (classes.py:156-232): the segment ending at vertex q
-    if (act) {
-      const int32_t yr = y0 + L.xn[ka][lane];
-      if (q > 0) {
-#pragma unroll
-        for (int r = 0; r < RMAX; r++)
-          if (r < P.n_rules)
-            rs[r].offer(P.rules[r], P.pre_threshold_mode, prev_year, yr - prev_year, prev_fit,
-                        prev_fit - fit_vertex, status);
-      }
-      prev_fit = fit_vertex;
-      prev_year = yr;
-    }
-    pm = cm;
-    pb = cb;
   }
 
   probe.mark(3);
@@ -895,18 +914,6 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
       return kDone;
     }
     return f32_bad ? kDeferWide : kDeferExact;
-  }
-  if (!ok) {  // the reference raises for this pixel: per-year fields of present years are NaN
-    for (uint64_t m = pres; m; m &= m - 1) {
-      const int64_t o = (int64_t)__builtin_ctzll(m) * os + p;
-      if (out.val_fit) out.val_fit[o] = nan;
-      if (out.fit_m) out.fit_m[o] = nan;
-      if (out.fit_b) out.fit_b[o] = nan;
-      if (out.right_m) out.right_m[o] = nan;
-      if (out.right_b) out.right_b[o] = nan;
-      if (out.spike) out.spike[o] = 0;
-      if (out.vertex) out.vertex[o] = 0;
-    }
   }
   if (out.n_years) out.n_years[p] = T;
   if (out.status) out.status[p] = status;
