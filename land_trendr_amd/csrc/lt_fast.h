@@ -574,7 +574,9 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
         iL = bl ? i : iL;
       };
       // a zero-residual start (worth fl(c + OPTa[i]) in the reference) on OPTa[i] of tag tg
-      // (tg < 0: inexact, tag unknown), in decreasing start order
+      // (tg < 0: inexact, tag unknown) after the pair below, in decreasing start order: rare
+      // (exactly collinear segments of >= 3 points), so kept general
+      double gh = inf;  // the group's upper end (early exit)
       auto zero_start = [&](int i, double v, int tg) __attribute__((always_inline)) {
         if (tg >= 0 && tg < 256) {  // exact
           if (v <= Ve) {
@@ -589,14 +591,39 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
           gi = i;
           gt = tg;
           gv = v;
+          gh = v + w;
         } else if (ord == 0) {
           track(i, v, v + w, v - w, tg < 0 ? -1 : tg + 1);
         }  // ord < 0: strictly above the group's best, never the first minimum
       };
-      // starts in decreasing order ("<=" keeps the smaller start among equal values). First the
-      // 1- and 2-point starts: residual exactly 0
-      zero_start(j, c + opt_j, tg_j);
-      if (j >= 1) zero_start(j - 1, c + opt_jm1, tg_jm1);  // wave-uniform condition
+      // the 1- and 2-point starts j and j-1 (residual exactly 0), select-based: the exact ones
+      // give Ve/ie (the smaller start wins ties); of the inexact ones the tag order keeps one in
+      // the group, and only two inexact starts of different bases leave one for the trackers
+      {
+        const bool has1 = j >= 1;  // wave-uniform
+        const double v0 = c + opt_j, v1s = c + opt_jm1;
+        const bool x0 = tg_j < 256, x1 = has1 && tg_jm1 < 256;
+        const bool g0 = !x0, g1 = has1 && !x1;
+        Ve = x0 ? v0 : inf;
+        ie = j;
+        if (x1 && v1s <= Ve) {
+          Ve = v1s;
+          ie = j - 1;
+        }
+        const int ord = (zok && g0 && g1) ? tag_order(tg_jm1, tg_j, v1s, c) : 0;
+        const bool pick1 = g1 && (!g0 || ord > 0);
+        gi = pick1 ? j - 1 : (g0 ? j : -1);
+        gt = pick1 ? tg_jm1 : tg_j;
+        gv = pick1 ? v1s : (g0 ? v0 : inf);
+        gh = gv + __builtin_fma(0x1p-50, __builtin_fabs(gv), Emax);
+        const bool left = g0 && g1 && ord == 0;  // start j-1 beside the group's start j
+        if (__ballot(left)) {
+          if (left) {
+            const double w = __builtin_fma(0x1p-50, __builtin_fabs(v1s), Emax);
+            track(j - 1, v1s, v1s + w, v1s - w, tg_jm1 + 1);
+          }
+        }
+      }
       // prefix bound for the early exit below: every segment ending at j has Syy <= SyyAll
       wx0 = L.xn[j][lane];
       wy0 = (double)L.ys[j][lane];
@@ -645,15 +672,24 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
       // fl(c + OPTa[i])) or an interval candidate that starts a new base if it wins
       auto offer = [&](int i, double o, int tg, double v, double hi, double lo, bool zr) __attribute__((always_inline)) {
         if (__ballot(zr)) {
-          if (zr) zero_start(i, c + o, tg);
+          if (zr) {
+            zero_start(i, c + o, tg);
+            hi = inf;  // kept out of the trackers (an infinite upper end never decides)
+            lo = inf;
+          }
         }
-        if (!zr) track(i, v, hi, lo, -1);
+        track(i, v, hi, lo, -1);
       };
-      // the group's upper end (for the early exit; inf while the group is empty)
-      auto group_hi = [&]() __attribute__((always_inline)) { return gv + __builtin_fma(0x1p-50, __builtin_fabs(gv), Emax); };
       // the 1- and 2-point starts (priced above) only add their points to the sums
       add_xy(wx0, wy0);
       if (j >= 1) add_xy(wx1, wy1);
+      // an upper bound on the column minimum so far (it only decreases as starts are added). A
+      // start whose lower end lies above it can change no decision: it is neither the smallest
+      // upper end nor among the lower ends at or below the final minimum bound H
+      auto upper = [&]() __attribute__((always_inline)) {
+        const double h = Hi < Ve ? Hi : Ve;
+        return gh < h ? gh : h;
+      };
       // the other starts two at a time: two independent pricing chains per iteration and one
       // exit test. Early exit (dp_start_bound): once no start below i can reach an upper bound on
       // the column minimum in any lane, the column is complete; a start priced past that point
@@ -669,14 +705,13 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
           add_xy(wx3, wy3);
           price(j - 3, opt_jm3, tg_jm3, vb, hb, lb, bb, zb);
         }
-        offer(j - 2, opt_jm2, tg_jm2, va, ha, la, za);
-        if (two) offer(j - 3, opt_jm3, tg_jm3, vb, hb, lb, zb);
-        if (prune) {
-          double Hb = Hi < Ve ? Hi : Ve;
-          const double gh = group_hi();
-          Hb = gh < Hb ? gh : Hb;
-          if (!__ballot(col && !(ba > Hb || (two && bb > Hb)))) more = false;
+        double Hb = upper();
+        if (__ballot(la <= Hb || (two && lb <= Hb))) {  // else neither can change a decision
+          offer(j - 2, opt_jm2, tg_jm2, va, ha, la, za);
+          if (two) offer(j - 3, opt_jm3, tg_jm3, vb, hb, lb, zb);
+          Hb = upper();
         }
+        if (prune && !__ballot(col && !(ba > Hb || (two && bb > Hb)))) more = false;
         more = more && two;
       }
       for (int ii = j - 4; more && ii >= 0; ii -= 2) {  // the rest from LDS / private memory
@@ -696,16 +731,16 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
           tb = ((exact >> (i - 1)) & 1) ? 0 : -1;
           price(i - 1, ob, tb, vb, hb, lb, bb, zb);
         }
-        offer(i, oa, ta, va, ha, la, za);
-        if (two) offer(i - 1, ob, tb, vb, hb, lb, zb);
-        if (prune) {
-          double Hb = Hi < Ve ? Hi : Ve;
-          const double gh = group_hi();
-          Hb = gh < Hb ? gh : Hb;
-          if (!__ballot(col && !(ba > Hb || (two && bb > Hb)))) break;
+        double Hb = upper();
+        if (__ballot(la <= Hb || (two && lb <= Hb))) {
+          offer(i, oa, ta, va, ha, la, za);
+          if (two) offer(i - 1, ob, tb, vb, hb, lb, zb);
+          Hb = upper();
         }
+        if (prune && !__ballot(col && !(ba > Hb || (two && bb > Hb)))) break;
       }
-      if (gi >= 0) {  // the group's best enters the trackers
+      // the group's best enters the trackers (an empty group: gv = inf, no effect)
+      {
         const double w = __builtin_fma(0x1p-50, __builtin_fabs(gv), Emax);
         track(gi, gv, gv + w, gv - w, gt + 1);
       }
