@@ -640,8 +640,10 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
       // start i (>= 3 points) priced from the current sums: value v, its interval [lo, hi] around
       // the reference value (tg: tag of OPTa[i]), the early-exit bound for the starts below, and
       // whether the segment is exactly collinear with a residual that rounds away (zr)
-      auto price = [&](int i, double o, int tg, double& v, double& hi, double& lo, double& bnd,
-                       bool& zr) __attribute__((always_inline)) {
+      // returns whether the interval reaches a zero residual (zero_test decides, where it can
+      // matter)
+      auto price = [&](int i, double o, int tg, double& v, double& hi, double& lo,
+                       double& bnd) __attribute__((always_inline)) {
         // closed-form SSE: (m*Syy - Sy^2 - N1^2/D) / m, one reciprocal
         const int m = j - i + 1;  // wave-uniform, >= 3
         const double md = (double)m;
@@ -661,12 +663,36 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
         hi = v + w;
         lo = v - w;
         bnd = dp_start_bound_slack(e, o, wopt, c, slack);
-        // the exact-zero test only where the interval reaches a zero residual
-        const bool near0 = zlane && e <= ws;
-        zr = false;
-        if (__ballot(near0)) {
-          if (near0) zr = kZero * Syy < 0x1p-54 * c && sse_exact_zero(t1, D, N1);
+        return zlane && e <= ws;
+      };
+      // exactly collinear with a residual that rounds away (lt_pixel.h kZero, sse_exact_zero), on
+      // sums of integer data (exact binary64 integers)
+      auto zero_test = [&](int m, int sx, int sxx, double sy, double sxy, double syy)
+                           __attribute__((always_inline)) {
+        const double md = (double)m;
+        const double D = (double)(m * sxx - sx * sx);
+        const double t1 = __builtin_fma(md, syy, -(sy * sy));
+        const double N1 = __builtin_fma(md, sxy, -((double)sx * sy));
+        return kZero * syy < 0x1p-54 * c && sse_exact_zero(t1, D, N1);
+      };
+      // the zero tests of starts a = i and b = i - 1 (b's point xb, yb is the last one added;
+      // a's sums are the current ones less that point, exact for the integer data tested):
+      // bit 0 for a, bit 1 for b
+      auto zero_tests = [&](int i, bool two, bool na, bool nb, int xb, double yb)
+                            __attribute__((always_inline)) {
+        int z = 0;
+        if (__ballot(na || (two && nb))) {
+          const int m = j - i + 1;
+          if (two) {
+            if (na && zero_test(m, Sx - xb, Sxx - xb * xb, Sy - yb,
+                                __builtin_fma(-(double)xb, yb, Sxy), __builtin_fma(-yb, yb, Syy)))
+              z |= 1;
+            if (nb && zero_test(m + 1, Sx, Sxx, Sy, Sxy, Syy)) z |= 2;
+          } else if (na && zero_test(m, Sx, Sxx, Sy, Sxy, Syy)) {
+            z |= 1;
+          }
         }
+        return z;
       };
       // a start of >= 3 points: a zero-residual start (v recomputed as the reference's
       // fl(c + OPTa[i])) or an interval candidate that starts a new base if it wins
@@ -698,17 +724,18 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
       if (more) {  // starts j-2 and j-3 from the register window
         const bool two = j >= 3;
         double va, ha, la, ba, vb = 0.0, hb = 0.0, lb = 0.0, bb = 0.0;
-        bool za, zb = false;
+        bool nb = false;
         add_xy(wx2, wy2);
-        price(j - 2, opt_jm2, tg_jm2, va, ha, la, ba, za);
+        const bool na = price(j - 2, opt_jm2, tg_jm2, va, ha, la, ba);
         if (two) {
           add_xy(wx3, wy3);
-          price(j - 3, opt_jm3, tg_jm3, vb, hb, lb, bb, zb);
+          nb = price(j - 3, opt_jm3, tg_jm3, vb, hb, lb, bb);
         }
         double Hb = upper();
         if (__ballot(la <= Hb || (two && lb <= Hb))) {  // else neither can change a decision
-          offer(j - 2, opt_jm2, tg_jm2, va, ha, la, za);
-          if (two) offer(j - 3, opt_jm3, tg_jm3, vb, hb, lb, zb);
+          const int z = zero_tests(j - 2, two, na, nb, wx3, wy3);
+          offer(j - 2, opt_jm2, tg_jm2, va, ha, la, z & 1);
+          if (two) offer(j - 3, opt_jm3, tg_jm3, vb, hb, lb, z & 2);
           Hb = upper();
         }
         if (prune && !__ballot(col && !(ba > Hb || (two && bb > Hb)))) more = false;
@@ -719,22 +746,26 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
         const bool two = i >= 1;                            // wave-uniform
         add_xy(L.xn[i][lane], (double)L.ys[i][lane]);
         double va, ha, la, ba, vb = 0.0, hb = 0.0, lb = 0.0, bb = 0.0;
-        bool za, zb = false;
+        bool nb = false;
         const double oa = OPTa[i];
         const int ta = ((exact >> i) & 1) ? 0 : -1;  // tags are kept in the window only
-        price(i, oa, ta, va, ha, la, ba, za);
+        const bool na = price(i, oa, ta, va, ha, la, ba);
         double ob = 0.0;
-        int tb = 0;
+        int tb = 0, xb = 0;
+        double yb = 0.0;
         if (two) {
-          add_xy(L.xn[i - 1][lane], (double)L.ys[i - 1][lane]);
+          xb = L.xn[i - 1][lane];
+          yb = (double)L.ys[i - 1][lane];
+          add_xy(xb, yb);
           ob = OPTa[i - 1];
           tb = ((exact >> (i - 1)) & 1) ? 0 : -1;
-          price(i - 1, ob, tb, vb, hb, lb, bb, zb);
+          nb = price(i - 1, ob, tb, vb, hb, lb, bb);
         }
         double Hb = upper();
         if (__ballot(la <= Hb || (two && lb <= Hb))) {
-          offer(i, oa, ta, va, ha, la, za);
-          if (two) offer(i - 1, ob, tb, vb, hb, lb, zb);
+          const int z = zero_tests(i, two, na, nb, xb, yb);
+          offer(i, oa, ta, va, ha, la, z & 1);
+          if (two) offer(i - 1, ob, tb, vb, hb, lb, z & 2);
           Hb = upper();
         }
         if (prune && !__ballot(col && !(ba > Hb || (two && bb > Hb)))) break;
