@@ -492,6 +492,15 @@ int lt_analyze_tiles_after(lt_ctx* c, const lt_scene* sc, const lt_params* prm, 
     tmp.order[k] = sc->order[k];
     tmp.dist[k] = sc->dist[k];
   }
+  for (int y = 0; y < Y; y++) {  // first obs (input order) at minimal |days|, as the kernels pick
+    int best = -1, bd = 0x7fffffff;
+    for (int k = tmp.slot_begin[y]; k < tmp.slot_begin[y + 1]; k++)
+      if (tmp.dist[k] < bd) {
+        bd = tmp.dist[k];
+        best = tmp.order[k];
+      }
+    tmp.winner_all[y] = best;
+  }
   if (!c->scene_valid || memcmp(&tmp, c->h_scene, sizeof tmp) != 0) {
     // an earlier call, possibly on another stream, may still be reading d_scene: its last tile's
     // resolve (side stream, in order, after every analyze it waited for) marks the end of all of

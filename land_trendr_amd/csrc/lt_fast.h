@@ -23,6 +23,11 @@
 #ifndef LT_RESOLVE_PRIV_MAXY
 #define LT_RESOLVE_PRIV_MAXY 48
 #endif
+// labels-only launches of up to this many rules take the certified path (closed-form fits, the
+// emulated ones only around the rules' candidates); more rules keep one emulated fit per vertex
+#ifndef LT_CERT_RULES
+#define LT_CERT_RULES 4
+#endif
 
 namespace lt {
 
@@ -136,6 +141,7 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
   uint64_t pres = 0;  // year slots with a winner: present point t is the t-th set bit
   bool f32_bad = false;
   bool intdata = true;  // every value an integer of int16 range (lt_pixel.h sse_exact_zero)
+  bool infdata = false;  // some value infinite (a binary32 series): the emulated fits fail (rc < 0)
   // years in batches of 8: the winners first, then their 8 value loads issued together (one
   // load per year in sequence would leave each wave waiting out the HBM latency 30 times)
   constexpr int WB = LT_WB;
@@ -146,12 +152,15 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
       const int y = yb + u;
       best[u] = -1;
       if (y >= Y) continue;  // wave-uniform
+      if (in.obs_valid == nullptr) {  // launch-uniform: no mask, the scene's winner
+        best[u] = live ? S.winner_all[y] : -1;
+        continue;
+      }
       int bd = 0x7fffffff;
       const int k1 = S.slot_begin[y + 1];
       for (int k = S.slot_begin[y]; k < k1; k++) {
         const int o = S.order[k];
-        const bool ok =
-            live && (in.obs_valid == nullptr || in.obs_valid[(int64_t)o * is + p] != 0);
+        const bool ok = live && in.obs_valid[(int64_t)o * is + p] != 0;
         if (ok && S.dist[k] < bd) {
           bd = S.dist[k];
           best[u] = o;
@@ -198,6 +207,7 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
         }
         if constexpr (!std::is_same<VT, int16_t>::value) {
           if (!(v == __builtin_rint(v) && __builtin_fabs(v) <= 32767.0)) intdata = false;
+          if (__builtin_isinf(v)) infdata = true;
         }
         L.ys[T][lane] = vs;
         pres |= 1ull << y;
@@ -854,14 +864,21 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
   if (year_out) {
     // Year-major: every year slot is one wave-uniform step and each per-year plane is written
     // one coalesced row at a time (lane l -> pixel p, all lanes the same year). A lane reaching
-    // a vertex that has a next vertex needs that segment's fit: one LAPACK-emulated fit per year
-    // for the lanes that need it (lanes without a next vertex reuse the previous equation,
-    // utils.py:662). Deferred and dead lanes write nothing (the resolve stage writes them).
+    // a vertex that has a next vertex needs that segment's fit (lanes without a next vertex reuse
+    // the previous equation, utils.py:662). The fits are LAPACK-emulated in lockstep, and each
+    // lane keeps one fit ahead: a fit step is issued only in a year where some lane reaches such
+    // a vertex with its lookahead slot empty, and in it every lane whose slot is free (or is being
+    // used this year) fits its next segment. A wave then issues about as many fit steps as its
+    // lanes have vertices (the lower bound), not one per year. Deferred and dead lanes write
+    // nothing (the resolve stage writes them).
     const bool emit = live && !deferred;
     const bool good = emit && ok;
     uint64_t vrem = vmask;           // vertices not reached yet (non-spike indices)
+    uint64_t frem = vmask;           // vertices whose segment is not fitted yet (the lowest next)
     double pm = 0.0, pb = 0.0;       // eqn of the previous vertex
     double cm = 0.0, cb = 0.0;       // eqn of the current vertex (right eqn of the points)
+    double nm = 0.0, nb = 0.0;       // lookahead: eqn of the segment from the next vertex
+    bool have_n = false;
     int t = 0, k = 0, q = 0;         // present index, non-spike index, vertex number
     for (int y = 0; y < Y; y++) {    // wave-uniform
       const bool pr = good && ((pres >> y) & 1);
@@ -869,20 +886,33 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
       const bool isv = pr && !sp && ((vrem >> k) & 1);
       const uint64_t after = vrem & (vrem - 1);  // vertices after this one
       const bool nextfit = isv && after != 0;
-      if (__ballot(nextfit)) {
-        const int kb = nextfit ? __builtin_ctzll(after) : k + 1;
-        const int kbase = nextfit ? k : 0;
-        double sm = 0.0, sbv = 0.0;
+      double sm = 0.0, sbv = 0.0;
+      bool fitnow = false;
+      if (__ballot(nextfit && !have_n)) {
+        const uint64_t fnext = frem & (frem - 1);
+        fitnow = fnext != 0 && (!have_n || nextfit);
+        const int kbase = fitnow ? __builtin_ctzll(frem) : 0;
+        const int kb = fitnow ? __builtin_ctzll(fnext) : 1;
         const int rc = lsq_fit_lockstep(
-            nextfit, kb - kbase + 1, [&](int i) { return (int)L.xn[kbase + i][lane]; },
+            fitnow, kb - kbase + 1, [&](int i) { return (int)L.xn[kbase + i][lane]; },
             [&](int i) { return (double)L.ys[kbase + i][lane]; }, xtab, sm, sbv);
-        if (nextfit) {
+        if (fitnow) {
           if (rc < 0) status |= LT_ST_NUMERIC;
-          pm = cm;
-          pb = cb;
-          cm = sm;
-          cb = sbv;
+          frem = fnext;
         }
+      }
+      if (nextfit) {
+        pm = cm;
+        pb = cb;
+        cm = have_n ? nm : sm;
+        cb = have_n ? nb : sbv;
+        have_n = have_n && fitnow;  // the slot was used: refilled by this year's step
+      } else {
+        have_n = have_n || fitnow;
+      }
+      if (have_n && fitnow) {
+        nm = sm;
+        nb = sbv;
       }
       if (isv && !nextfit) {  // the last vertex: left eqn = right eqn = the previous one
         pm = cm;
@@ -918,6 +948,158 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
         if (!sp) k++;
         t++;
       }
+    }
+  } else if constexpr (!EXACT && RMAX <= LT_CERT_RULES) {
+    // ---- labels only, certified. The rules need the fitted values at the vertices, and only the
+    // winners' values bit-exactly. (A) lockstep over the vertex number q: each segment's fit by
+    // the closed form, the fitted value at each vertex as an interval around the reference's
+    // (kFitW), and each disturbance offered to the rules' candidate sets (lt_pixel.h RuleCands);
+    // (B) lockstep over the candidates: the emulated (reference) fits of the two or three
+    // segments around each, and the exact offers, in order, to the rules holding it ----
+    const int nv = __builtin_popcountll(vmask);
+    const int nvmax = wave_max(nv);
+    RuleCands cand[RMAX];
+    uint64_t vrem = vmask;  // vertices from q on: vertex q is its lowest bit
+    // closed-form eqn (slope, intercept, error scale) of the segment ending at vertex q-1
+    double am = 0.0, ab = 0.0, asc = 0.0;
+    double fprev = 0.0, wprev = 0.0;  // fitted value of vertex q-1: center, half-width
+    int32_t yprev = 0;
+    auto add_pt = [&](int k, int& Sx, int& Sxx, double& Sy, double& Sxy, double& ymx)
+                      __attribute__((always_inline)) {
+      const int xi = L.xn[k][lane];
+      const double yi = (double)L.ys[k][lane];
+      Sx += xi;
+      Sxx += xi * xi;
+      Sy += yi;
+      Sxy = __builtin_fma((double)xi, yi, Sxy);
+      ymx = __builtin_fmax(ymx, __builtin_fabs(yi));
+    };
+    for (int q = 0; q < nvmax; q++) {
+      const bool act = q < nv;
+      const int ka = act ? __builtin_ctzll(vrem) : 0;
+      if (act) vrem &= vrem - 1;
+      const bool has_next = act && q + 1 < nv;
+      const int kb = has_next ? __builtin_ctzll(vrem) : ka;
+      double cm = am, cb = ab, csc = asc;  // the last vertex reuses the previous eqn (utils.py:662)
+      if (__ballot(has_next)) {
+        // least squares of the points ka..kb by the closed form: two to four points straight-line,
+        // longer segments in a loop the wave takes only if some lane has one
+        const int m = kb - ka + 1;
+        int Sx = 0, Sxx = 0;
+        double Sy = 0.0, Sxy = 0.0, ymx = 0.0;
+        if (has_next) {
+          add_pt(ka, Sx, Sxx, Sy, Sxy, ymx);
+          add_pt(ka + 1, Sx, Sxx, Sy, Sxy, ymx);
+          if (m >= 3) add_pt(ka + 2, Sx, Sxx, Sy, Sxy, ymx);
+          if (m >= 4) add_pt(ka + 3, Sx, Sxx, Sy, Sxy, ymx);
+        }
+        const bool longer = has_next && m > 4;
+        if (__ballot(longer)) {
+          const int mmax = wave_max(longer ? m : 0);
+          for (int k = 4; k < mmax; k++)
+            if (k < m) add_pt(ka + k, Sx, Sxx, Sy, Sxy, ymx);
+        }
+        if (has_next) {
+          const double md = (double)m;
+          const double D = (double)(m * Sxx - Sx * Sx);  // > 0: distinct x
+          const double N1 = __builtin_fma(md, Sxy, -((double)Sx * Sy));
+          double r = __builtin_amdgcn_rcp(D);
+          r = __builtin_fma(r, __builtin_fma(-D, r, 1.0), r);
+          double rm = __builtin_amdgcn_rcp(md);
+          rm = __builtin_fma(rm, __builtin_fma(-md, rm, 1.0), rm);
+          cm = N1 * r;
+          cb = __builtin_fma(-cm, (double)Sx, Sy) * rm;
+          csc = __builtin_fma(__builtin_fabs(cm), 64.0, __builtin_fabs(cb)) + ymx;
+        }
+      }
+      // the fitted value at vertex q (eqns2fitted_points: the closer of the left and right eqn)
+      const double x = act ? (double)L.xn[ka][lane] : 0.0;
+      const double raw_v = act ? (double)L.ys[ka][lane] : 0.0;
+      const double fr = (cm * x) + cb, wr = kFitW * csc;
+      double fv = fr, w = wr;
+      if (q > 0 && has_next) {
+        const double fl = (am * x) + ab, wl = kFitW * asc;
+        const double dl = __builtin_fabs(fl - raw_v), dr = __builtin_fabs(fr - raw_v);
+        const double slack = wl + wr + 0x1p-50 * (dl + dr);
+        if (dl + slack <= dr) {  // certainly the left eqn
+          fv = fl;
+          w = wl;
+        } else if (!(dr + slack < dl)) {  // either: the hull of both intervals
+          const double lo = __builtin_fmin(fl - wl, fr - wr), hi = __builtin_fmax(fl + wl, fr + wr);
+          fv = 0.5 * (lo + hi);
+          w = 0.5 * (hi - lo) + 0x1p-50 * (__builtin_fabs(lo) + __builtin_fabs(hi));
+        }
+      }
+      const int32_t yr = y0 + (int32_t)x;
+      if (act && q > 0) {  // the disturbance from vertex q-1 to vertex q (classes.py:156-176)
+        const double mag = fprev - fv;
+        const double wm = (wprev + w) + 0x1p-50 * (__builtin_fabs(fprev) + __builtin_fabs(fv));
+#pragma unroll
+        for (int r = 0; r < RMAX; r++)
+          if (r < P.n_rules)
+            cand[r].offer(P.rules[r], P.pre_threshold_mode, yprev, yr - yprev, fprev - wprev,
+                          fprev + wprev, mag - wm, mag + wm, 1ull << ka, status);
+      }
+      am = cm;
+      ab = cb;
+      asc = csc;
+      fprev = fv;
+      wprev = w;
+      yprev = yr;
+    }
+    // (B) the candidates in increasing order; a series with an infinite value (whose emulated
+    // fits fail and are flagged) replays every disturbance
+    uint64_t U = 0;
+#pragma unroll
+    for (int r = 0; r < RMAX; r++)
+      if (r < P.n_rules) U |= cand[r].G;
+    if (infdata) U = vmask & (vmask - 1);
+    const int nu = __builtin_popcountll(U);
+    const int numax = wave_max(nu);
+    for (int it = 0; it < numax; it++) {
+      const bool act = it < nu;
+      const int kq = act ? __builtin_ctzll(U) : 1;  // end vertex of the disturbance (>= 1)
+      if (act) U &= U - 1;
+      const uint64_t below = act ? vmask & ((1ull << kq) - 1) : 1;  // the vertices before kq
+      const int k1 = 63 - __builtin_clzll(below);                     // vertex q-1
+      const uint64_t below2 = below & ~(1ull << k1);
+      const bool has2 = act && below2 != 0;
+      const int k2 = has2 ? 63 - __builtin_clzll(below2) : 0;         // vertex q-2
+      const uint64_t above = act ? vmask & ~((2ull << kq) - 1) : 0;    // (kq = 63: none)
+      const bool hasn = above != 0;
+      const int kn = hasn ? __builtin_ctzll(above) : 0;               // vertex q+1
+      // the reference's eqns (vertices2eqns, utils.py:646-669): e1 of segment q-1 (k1..kq),
+      // e2 of segment q-2 (k2..k1), e3 of segment q (kq..kn)
+      double m1 = 0.0, b1 = 0.0, m2 = 0.0, b2 = 0.0, m3 = 0.0, b3 = 0.0;
+      auto fit = [&](bool on, int k0, int k9, double& sm, double& sb) __attribute__((always_inline)) {
+        if (__ballot(on)) {
+          const int rc = lsq_fit_lockstep(
+              on, k9 - k0 + 1, [&](int i) { return (int)L.xn[k0 + i][lane]; },
+              [&](int i) { return (double)L.ys[k0 + i][lane]; }, xtab, sm, sb);
+          if (on && rc < 0) status |= LT_ST_NUMERIC;
+        }
+      };
+      fit(act, k1, kq, m1, b1);
+      fit(has2, k2, k1, m2, b2);
+      fit(hasn, kq, kn, m3, b3);
+      // fitted values at vertices q-1 and q, as the walk computes them
+      auto vfit = [&](int k, bool two, double pm, double pb, double cm, double cb)
+                      __attribute__((always_inline)) {
+        const double xv = (double)L.xn[k][lane];
+        const double fr = (cm * xv) + cb;
+        if (!two || (pm == cm && pb == cb)) return fr;
+        const double fl = (pm * xv) + pb;
+        const double raw_v = (double)L.ys[k][lane];
+        return __builtin_fabs(fl - raw_v) <= __builtin_fabs(fr - raw_v) ? fl : fr;
+      };
+      const double f1 = vfit(k1, has2, m2, b2, m1, b1);
+      const double fq = hasn ? vfit(kq, true, m1, b1, m3, b3) : (m1 * (double)L.xn[kq][lane]) + b1;
+      const int32_t on = y0 + (int32_t)L.xn[k1][lane];
+      const int32_t du = (int32_t)L.xn[kq][lane] - (int32_t)L.xn[k1][lane];
+#pragma unroll
+      for (int r = 0; r < RMAX; r++)
+        if (r < P.n_rules && act && (infdata || ((cand[r].G >> kq) & 1)))
+          rs[r].offer(P.rules[r], P.pre_threshold_mode, on, du, f1, f1 - fq, status);
     }
   } else {
     // labels only, in lockstep over the vertex number q: the fitted value at each vertex is all

@@ -26,6 +26,9 @@ struct DevScene {
   uint8_t feb29_bad[LT_MAX_YEARS];
   int32_t order[LT_MAX_OBS];
   int32_t dist[LT_MAX_OBS];
+  // pick_winners' winner per year slot when every observation is valid (no cloud mask): the same
+  // for all pixels, so computed once per scene on the host (-1: no observation in the year)
+  int32_t winner_all[LT_MAX_YEARS];
 };
 
 // numpy pairwise sum (n <= 128) of a[0..n-1]: 8 accumulators, then sequential remainder.
@@ -92,6 +95,69 @@ struct RuleState1 {
     if (out.initial_val) out.initial_val[q] = init;
   }
 };
+
+// Vertex fitted values known only to within an interval (the labels-only analyze path prices
+// every segment fit with the closed form first, lt_fast.h): the candidate set of ONE rule. match_rule
+// (classes.py:185-230) keeps, among the matching disturbances, the first one of maximal key
+// (GD: magnitude; LD: duration; FD: -onset, onsets increase along the trendline). Offered the
+// disturbances in order, each with an interval [klo, khi] around its key and a match that is
+// certain or only possible (a pre_threshold test the init interval straddles), G collects every
+// disturbance that can still be the winner:
+//   * khi <= lo (lo: the largest lower end among CERTAIN matches in G) -> an earlier certain match
+//     is at least as large: never the first maximum;
+//   * a certain match with klo > hi (hi: the largest upper end in G) -> larger than all of G, so
+//     no member of G can win: G restarts from it;
+//   * otherwise it joins G.
+// The winner is always in G, so replaying the exact offers over G alone (RuleState1, in order)
+// gives the reference's winner. G is a mask over the disturbance's end-vertex index.
+struct RuleCands {
+  uint64_t G = 0;
+  double lo = -__builtin_inf(), hi = -__builtin_inf();
+
+  __host__ __device__ __attribute__((always_inline)) void offer(
+      const lt_rule& R, int pre_mode, int32_t d_on, int32_t d_du, double init_lo,
+      double init_hi, double mag_lo, double mag_hi, uint64_t bit, int& status) {
+    bool match = true, maybe = false;
+    if (R.onset_op == LT_Q_EQ) match = match && ((double)d_on == R.onset_val);
+    else if (R.onset_op == LT_Q_LE) match = match && !((double)d_on > R.onset_val);
+    else if (R.onset_op == LT_Q_GE) match = match && !((double)d_on < R.onset_val);
+    if (R.duration_op == LT_Q_GT) match = match && !((double)d_du <= R.duration_val);
+    else if (R.duration_op == LT_Q_LT) match = match && !((double)d_du >= R.duration_val);
+    if (R.pre_op != LT_Q_UNSET) {
+      if (pre_mode == LT_PRE_REFERENCE) {
+        status |= LT_ST_PRE_THRESHOLD_ATTR;
+      } else if (R.pre_op == LT_Q_GT) {  // match iff !(init <= pre_val)
+        const bool yes = init_lo > R.pre_val, no = init_hi <= R.pre_val;
+        match = match && !no;
+        maybe = maybe || !yes;
+      } else if (R.pre_op == LT_Q_LT) {  // match iff !(init >= pre_val)
+        const bool yes = init_hi < R.pre_val, no = init_lo >= R.pre_val;
+        match = match && !no;
+        maybe = maybe || !yes;
+      }
+    }
+    if (!match) return;
+    double klo = mag_lo, khi = mag_hi;
+    if (R.change_type == LT_CT_FD) klo = khi = -(double)d_on;
+    else if (R.change_type == LT_CT_LD) klo = khi = (double)d_du;
+    if (khi <= lo) return;
+    if (!maybe && klo > hi) {
+      G = bit;
+      lo = klo;
+      hi = khi;
+      return;
+    }
+    G |= bit;
+    hi = khi > hi ? khi : hi;
+    if (!maybe) lo = klo > lo ? klo : lo;
+  }
+};
+
+// Half-width factor of a closed-form vertex fit against the reference's (emulated dgelsd) one:
+// |fitted value - reference fitted value| <= kFitW * (|slope| * 64 + |intercept| + max|y|) at any
+// year offset x < 64. tests/test_screening.py measures the emulated dgelsd and the kernel's closed
+// form against the exact rational fit over adversarial segments and requires a 2^10 margin.
+constexpr double kFitW = 0x1p-32;
 
 // change_labeling state for all rules (classes.py:213-230 winner bookkeeping).
 struct RuleState {

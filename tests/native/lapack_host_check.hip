@@ -126,3 +126,27 @@ extern "C" int ltx_lsq_small_vs_general(int m, const double* x, const double* y,
   out4[3] = c1;
   return (a + 8) * 16 + (b + 8);
 }
+
+// lt_pixel.h RuleCands against the full replay: n disturbances (onset, duration, exact init and
+// magnitude, half-widths of the intervals the candidate pass sees) offered to rule R. Returns 1
+// when replaying RuleState1 over the candidate set alone gives the full replay's winner (every
+// field bit-equal and the same status), 0 otherwise; *n_cand = size of the candidate set.
+extern "C" int ltx_rule_cands(int n, const int32_t* on, const int32_t* du, const double* init,
+                              const double* mag, const double* w_init, const double* w_mag,
+                              const lt_rule* R, int pre_mode, int* n_cand) {
+  lt::RuleState1 full, part;
+  lt::RuleCands cand;
+  int st_full = 0, st_cand = 0, st_part = 0;
+  for (int i = 0; i < n; i++) {
+    full.offer(*R, pre_mode, on[i], du[i], init[i], mag[i], st_full);
+    cand.offer(*R, pre_mode, on[i], du[i], init[i] - w_init[i], init[i] + w_init[i],
+               mag[i] - w_mag[i], mag[i] + w_mag[i], 1ull << i, st_cand);
+  }
+  for (int i = 0; i < n; i++)
+    if ((cand.G >> i) & 1) part.offer(*R, pre_mode, on[i], du[i], init[i], mag[i], st_part);
+  *n_cand = __builtin_popcountll(cand.G);
+  auto same = [](double a, double b) { return __builtin_memcmp(&a, &b, sizeof a) == 0; };
+  return full.have == part.have && full.on == part.on && full.du == part.du &&
+         same(full.mag, part.mag) && same(full.init, part.init) &&
+         (n == 0 || st_cand == st_full);
+}

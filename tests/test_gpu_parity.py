@@ -390,3 +390,64 @@ def test_analyze_tiles_batch_equals_single_tiles_and_oracle(engine):
             same = ((w.view(np.int64) == x.view(np.int64)) | (np.isnan(w) & np.isnan(x))
                     if w.dtype.kind == 'f' else w == x)
             assert same.all(), (a, b, f, int((~same).sum()))
+
+
+def _label_datasets():
+    """(name, dates, values [K, P] float64, rules, mode) for the labels-only test below."""
+    import datetime as dt
+    rng = np.random.default_rng(777)
+    T, P = 30, 4096
+    dates = [dt.date(1990 + t, 7, 1) for t in range(T)]
+    sets = []
+    # small-integer plateaus: 2-point segments whose fitted values sit ON the pre_threshold
+    # values and equal-magnitude disturbances (exact ties the closed form cannot order)
+    kind = rng.integers(0, 3, P)
+    v = np.where(kind[None, :] == 0, rng.integers(0, 4, (T, P)) * 100,
+                 np.where(kind[None, :] == 1, np.cumsum(rng.integers(-1, 2, (T, P)), 0) * 50,
+                          (np.arange(T)[:, None] % rng.integers(2, 5, P)[None, :]) * 100))
+    rules = [{'name': 'gd', 'val': 1, 'change_type': 'GD', 'pre_threshold': ['>', 100]},
+             {'name': 'fd', 'val': 2, 'change_type': 'FD', 'pre_threshold': ['<', 200]},
+             {'name': 'ld', 'val': 3, 'change_type': 'LD', 'duration': ['<', 3],
+              'pre_threshold': ['>', 0]},
+             {'name': 'gd2', 'val': 4, 'change_type': 'GD', 'onset_year': ['>=', 2000]}]
+    for lc in (1e-4, 0.5, 10.0):
+        sets.append(('plateaus-lc%g' % lc, dates, v.astype(np.float64), lc, rules, 'documented'))
+    sets.append(('plateaus-reference-mode', dates, v.astype(np.float64), 0.5, rules, 'reference'))
+    # the synthetic generator's series (c2 shape) with three rules
+    from land_trendr_amd.synth import make_scene
+    sc = make_scene(P, n_years=T, seed=778)
+    sets.append(('synthetic', sc.dates, sc.values.numpy(), 10.0, rules[:3], 'documented'))
+    # non-integer and large-offset values (closed-form error scale)
+    base = np.round(rng.normal(0, 40, (T, P)))
+    trend = np.where(np.arange(T)[:, None] > rng.integers(3, 25, P)[None, :], -300.0, 0.0)
+    sets.append(('eighths', dates, (1000 + base + trend) + rng.integers(0, 8, (T, P)) / 8.0, 0.5,
+                 rules[:1], 'documented'))
+    sets.append(('offset1e6', dates, 1e6 + base + trend, 10.0, rules[:1], 'documented'))
+    return sets
+
+
+@pytest.mark.parametrize('ds', range(7))
+def test_labels_only_launch_matches_oracle_and_full_launch(engine, ds):
+    """Labels-only launches take the certified path (closed-form vertex fits as intervals, the
+    emulated fits only around the rules' candidates, lt_fast.h): their rule rasters and status must
+    equal, bit for bit, the oracle's and those of a launch that also writes the trendline planes
+    (every vertex fit emulated). Datasets aim at the certified path's decisions: equal-magnitude
+    disturbances, fitted values equal to the pre_threshold values, FD/GD/LD rules with filters."""
+    from oracle import oracle
+    name, dates, vals, lc, rules, mode = _label_datasets()[ds]
+    meta = build_scene(dates, parse_date('2014-07-01'))
+    params, _ = compile_params(lc, rules, mode)
+    fields = ('status', 'matched', 'class_val', 'onset_year', 'duration', 'magnitude',
+              'initial_val')
+    dev = engine.device
+    v = torch.from_numpy(np.ascontiguousarray(vals)).to(dev)
+    lab = engine.analyze_tile(meta, params, v, None, fields)
+    full = engine.analyze_tile(meta, params, v, None)
+    torch.cuda.synchronize()
+    want = oracle.analyze_tile(meta, params, vals, None, n_threads=os.cpu_count() or 1)
+    for f in fields:
+        a, b, c = want[f], lab[f].cpu().numpy(), full[f].cpu().numpy()
+        for got, what in ((b, 'labels-only vs oracle'), (c, 'full vs oracle')):
+            same = ((a.view(np.int64) == got.view(np.int64)) | (np.isnan(a) & np.isnan(got))
+                    if a.dtype.kind == 'f' else a == got)
+            assert same.all(), (name, what, f, int((~same).sum()))

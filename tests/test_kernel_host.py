@@ -131,3 +131,43 @@ def test_lazy_dp_with_zero_residual_groups_matches_exact_dp(hc):
         assert _vertices(a1, n) == _vertices(a2, n), (list(xs), list(ys), c)
     print('lazy DP decided %d series, deferred %d' % (n_dec, n_def))
     assert n_dec > 4000
+
+
+def test_rule_candidates_replay_gives_the_full_winner(hc):
+    """lt_pixel.h RuleCands (the labels-only certified path): replaying match_rule's exact offers
+    over the candidate set alone gives the winner of replaying every disturbance, for FD/GD/LD
+    rules with onset/duration/pre_threshold filters, tie-heavy keys, init values straddling the
+    threshold, and intervals of zero to large width around the exact values."""
+    f64p, i32p = _abi.c_f64p, _abi.c_i32p
+    hc.ltx_rule_cands.argtypes = [ctypes.c_int, i32p, i32p, f64p, f64p, f64p, f64p,
+                                  ctypes.POINTER(_abi.LtRule), ctypes.c_int,
+                                  ctypes.POINTER(ctypes.c_int)]
+    rng = np.random.default_rng(17)
+    n_cand = ctypes.c_int()
+    sizes = []
+    for case in range(6000):
+        n = int(rng.integers(0, 20))
+        on = np.sort(rng.choice(np.arange(1985, 2025), n, replace=False)).astype(np.int32)
+        du = rng.integers(1, 4, n).astype(np.int32)
+        init = rng.choice([100.0, 100.5, 250.0, 400.0], n) + rng.integers(-2, 3, n) * 0.25
+        mag = rng.choice([-50.0, 0.0, 25.0, 25.0 + 2 ** -40, 80.0, 80.0], n)
+        scale = [0.0, 2.0 ** -40, 1e-3, 0.3, 30.0][case % 5]
+        w_init = rng.uniform(0, 1, n) * scale
+        w_mag = rng.uniform(0, 1, n) * scale
+        R = _abi.LtRule()
+        R.change_type = int(rng.integers(1, 4))
+        R.onset_op = int(rng.choice([_abi.LT_Q_UNSET, _abi.LT_Q_EQ, _abi.LT_Q_LE, _abi.LT_Q_GE]))
+        R.onset_val = float(rng.integers(1990, 2020))
+        R.duration_op = int(rng.choice([_abi.LT_Q_UNSET, _abi.LT_Q_GT, _abi.LT_Q_LT]))
+        R.duration_val = float(rng.integers(1, 4))
+        R.pre_op = int(rng.choice([_abi.LT_Q_UNSET, _abi.LT_Q_GT, _abi.LT_Q_LT]))
+        R.pre_val = float(rng.choice([100.0, 100.5, 250.0]))
+        mode = int(rng.choice([_abi.LT_PRE_REFERENCE, _abi.LT_PRE_DOCUMENTED]))
+        args = [np.ascontiguousarray(a) for a in (on, du, init, mag, w_init, w_mag)]
+        ok = hc.ltx_rule_cands(n, args[0].ctypes.data_as(i32p), args[1].ctypes.data_as(i32p),
+                               *[a.ctypes.data_as(f64p) for a in args[2:]], ctypes.byref(R),
+                               mode, ctypes.byref(n_cand))
+        assert ok == 1, (case, n, R.change_type, R.onset_op, R.duration_op, R.pre_op, mode)
+        sizes.append(n_cand.value)
+    # exact intervals leave (nearly) one candidate per rule
+    assert np.mean(sizes[0::5]) <= 1.5

@@ -218,3 +218,89 @@ def test_exact_zero_test_is_exact_on_int16_segments():
     for x, y in segs:
         exact, _ = exact_sse(x, y)
         assert sse_exact_zero(x, y) == (exact == 0), (x, y, exact)
+
+
+K_FITW = 2.0 ** -32  # lt_pixel.h kFitW
+
+
+def closed_form_fit(x, y):
+    """lt_fast.h labels-only pass A: the closed-form slope and intercept of a segment (sums from
+    its first point on, fma for Sxy; reciprocals of D and m within an ulp: exact roundings here,
+    the difference is counted in the margin) and its error scale |slope|*64 + |icpt| + max|y|."""
+    Sx = Sxx = 0
+    Sy = Sxy = 0.0
+    for xi, yi in zip(x, y):
+        Sx += int(xi)
+        Sxx += int(xi) * int(xi)
+        Sy = Sy + yi
+        Sxy = fma(float(xi), yi, Sxy)
+    m = len(x)
+    md = float(m)
+    D = float(m * Sxx - Sx * Sx)
+    N1 = fma(md, Sxy, -(float(Sx) * Sy))
+    sm = N1 * float(F(1) / F(D))
+    sb = fma(-sm, float(Sx), Sy) * float(F(1) / F(m))
+    scale = fma(abs(sm), 64.0, abs(sb)) + max(abs(v) for v in y)
+    return sm, sb, scale
+
+
+def fit_segments(seed):
+    """Segments as the vertex fits see them: 2 to 64 points, x offsets up to 63 (late, short
+    segments are the worst conditioned), the value patterns of segments() above."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for m in [2, 2, 2, 3, 3, 4, 4, 5, 8, 13, 30, 64]:
+        for gaps in (False, True):
+            if gaps and m <= 21:
+                x = np.sort(rng.choice(64, m, replace=False))
+            else:
+                x0 = int(rng.integers(0, 64 - m + 1))
+                x = np.arange(x0, x0 + m)
+            x = [int(v) for v in x]
+            ys = [
+                [float(v) for v in rng.integers(-32768, 32768, m)],
+                [float(v) for v in 1200 - 3 * np.arange(m) + np.round(rng.normal(0, 40, m))],
+                [float(np.float32(v)) for v in rng.normal(0.3, 0.2, m)],
+                [1e6 + float(v) for v in rng.integers(-3, 4, m)],
+                [float(np.float32(v)) for v in 1e5 + rng.uniform(0, 1e-3, m)],
+                [7.0 + 3.5 * xi for xi in x],
+                [float(v) for v in rng.integers(-1, 2, m)],
+                [0.0] * (m - 1) + [1.0],
+            ]
+            for y in ys:
+                out.append((x, y))
+    return out
+
+
+def test_fit_bound_holds_with_margin():
+    """kFitW: the labels-only path prices every vertex fit with the closed form and carries the
+    fitted value at a vertex as an interval of half-width kFitW * scale around the reference's;
+    the winners are then re-fitted with the emulated dgelsd. Sound if the reference's fitted value
+    (emulated dgelsd eqn, evaluated as fl(fl(m*x) + b)) and the closed form's lie within
+    kFitW * scale of each other at every x of the segment. Requires a 2^10 margin."""
+    worst = worst_ref = 0.0
+    n = 0
+    for seed in range(40):
+        for x, y in fit_segments(seed):
+            rc, slope, icpt, _ = oracle.lstsq(np.array(x, float), np.array(y, float))
+            assert rc == 0
+            cm, cb, scale = closed_form_fit(x, y)
+            m = len(x)
+            Sx, Sy = sum(F(v) for v in x), sum(F(v) for v in y)
+            D = m * sum(F(v) * F(v) for v in x) - Sx * Sx
+            se = (m * sum(F(a) * F(b) for a, b in zip(x, y)) - Sx * Sy) / D
+            be = (Sy - se * Sx) / m
+            for xv in x:
+                ref = slope * xv + icpt
+                cf = cm * xv + cb
+                if scale == 0:  # all-zero values: both fits are 0 (DGELSD's B == 0 shortcut)
+                    assert ref == 0 and cf == 0
+                    continue
+                worst = max(worst, abs(ref - cf) / scale)
+                worst_ref = max(worst_ref, float(abs(F(ref) - (se * xv + be)) / F(scale)))
+                assert abs(ref - cf) <= K_FITW * MARGIN * scale, (x, y, xv, ref, cf, scale)
+            n += 1
+    assert n > 3000
+    print('segments %d: |reference fit - closed form|/scale <= 2^%.1f, |reference - exact|/scale '
+          '<= 2^%.1f (kFitW 2^-32)' % (n, math.log2(worst or 2.0 ** -99),
+                                       math.log2(worst_ref or 2.0 ** -99)))
