@@ -55,13 +55,14 @@ __global__ __launch_bounds__(64, (MAXY <= 32 && RMAX == 1) ? LT_FAST_WAVES_C2 : 
                                                           const lt_tile_out out,
                                                           const lt::lsq_xf* __restrict__ xtab,
                                                           int64_t* __restrict__ defer,
-                                                          unsigned long long* __restrict__ n_defer) {
+                                                          unsigned long long* __restrict__ n_defer,
+                                                          uint64_t* __restrict__ yflags) {
   __shared__ lt::WaveLds<MAXY, VT, false> L;
   const int lane = threadIdx.x;
   const int64_t p = (int64_t)blockIdx.x * 64 + lane;
   const bool live = p < in.n_pix;
-  const int d = lt::analyze_fast<MAXY, RMAX, false, VT>(*S, P, in, out, xtab, p, live, lane, L,
-                                                        LT_ANALYZE_PROBE{});
+  const int d = lt::analyze_fast<MAXY, RMAX, false, VT>(*S, P, in, out, xtab, yflags, p, live,
+                                                        lane, L, LT_ANALYZE_PROBE{});
   // two lists: [0, n_pix) for the binary32 resolve, [n_pix, 2 n_pix) for the binary64 one;
   // counters [0] / [2] count them (wave-aggregated atomics)
   defer_append(live && d == lt::kDeferExact, p, lane, defer, &n_defer[0]);
@@ -77,7 +78,8 @@ __global__ __launch_bounds__(64) void resolve_fast_kernel(const lt::DevScene* __
                                                           const lt_tile_out out,
                                                           const lt::lsq_xf* __restrict__ xtab,
                                                           const int64_t* __restrict__ defer,
-                                                          unsigned long long* __restrict__ counters) {
+                                                          unsigned long long* __restrict__ counters,
+                                                          uint64_t* __restrict__ yflags) {
   __shared__ lt::WaveLds<MAXY, VT, true> L;
   const int lane = threadIdx.x;
   const int64_t n = (int64_t)counters[0];  // written by stage 1, a previous launch
@@ -89,8 +91,8 @@ __global__ __launch_bounds__(64) void resolve_fast_kernel(const lt::DevScene* __
     if (base >= n) break;
     const int64_t k = base + lane;
     const bool live = k < n;
-    lt::analyze_fast<MAXY, RMAX, true, VT>(*S, P, in, out, xtab, live ? defer[k] : 0, live, lane,
-                                           L);
+    lt::analyze_fast<MAXY, RMAX, true, VT>(*S, P, in, out, xtab, yflags, live ? defer[k] : 0,
+                                           live, lane, L);
   }
 }
 
@@ -106,6 +108,54 @@ __global__ __launch_bounds__(kBlock) void build_xtable_kernel(lt::lsq_xf* __rest
   else
     f.rc = -4;  // no x-set maps here
   xtab[idx] = f;
+}
+
+// The spike / vertex planes from the per-pixel year flags the analyze and resolve stages leave
+// (lt_fast.h): four pixels per thread, so each year row of a wave is one 256-byte store per plane
+// (a wave of the analyze kernel would write 64-byte pieces, which cost far more than their bytes).
+// V4: the planes and their stride are 4-byte aligned (else one pixel per thread).
+template <bool V4>
+__global__ __launch_bounds__(kBlock) void year_flags_kernel(const uint64_t* __restrict__ yflags,
+                                                            int64_t n, int Y,
+                                                            uint8_t* __restrict__ spike,
+                                                            uint8_t* __restrict__ vertex,
+                                                            int64_t os) {
+  const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if constexpr (V4) {
+    const int64_t p = t * 4;
+    if (p >= n) return;
+    const int np = n - p < 4 ? (int)(n - p) : 4;
+    uint64_t sf[4] = {0, 0, 0, 0}, vf[4] = {0, 0, 0, 0};
+    for (int i = 0; i < np; i++) {
+      sf[i] = yflags[p + i];
+      vf[i] = yflags[n + p + i];
+    }
+    for (int y = 0; y < Y; y++) {
+      uint32_t a = 0, b = 0;
+      for (int i = 0; i < 4; i++) {
+        a |= (uint32_t)((sf[i] >> y) & 1) << (8 * i);
+        b |= (uint32_t)((vf[i] >> y) & 1) << (8 * i);
+      }
+      const int64_t o = (int64_t)y * os + p;
+      if (np == 4) {
+        if (spike) *(uint32_t*)(spike + o) = a;
+        if (vertex) *(uint32_t*)(vertex + o) = b;
+      } else {
+        for (int i = 0; i < np; i++) {
+          if (spike) spike[o + i] = (uint8_t)(a >> (8 * i));
+          if (vertex) vertex[o + i] = (uint8_t)(b >> (8 * i));
+        }
+      }
+    }
+  } else {
+    if (t >= n) return;
+    const uint64_t sf = yflags[t], vf = yflags[n + t];
+    for (int y = 0; y < Y; y++) {
+      const int64_t o = (int64_t)y * os + t;
+      if (spike) spike[o] = (uint8_t)((sf >> y) & 1);
+      if (vertex) vertex[o] = (uint8_t)((vf >> y) & 1);
+    }
+  }
 }
 
 // waves of resolve_fast_kernel<MAXY, RMAX, VT> the device holds at once
@@ -199,6 +249,7 @@ struct lt_ctx {
   size_t used = 0;               // pairs recorded since the last stage_ms call
   int64_t launches = 0;
   int64_t* d_defer = nullptr;    // deferred-pixel list of the resolve stage
+  uint64_t* d_yflags = nullptr;  // per-pixel spike / vertex year flags (2 sets x 2 planes)
   unsigned long long* d_ndefer = nullptr;
   int64_t defer_cap = 0;
   lt::lsq_xf* d_xtab = nullptr;  // x-set factor table (built at context creation)
@@ -296,6 +347,7 @@ int lt_ctx_destroy(lt_ctx* c) {
     if (c->ev_resolved[s]) (void)hipEventDestroy(c->ev_resolved[s]);
   }
   if (c->d_defer) (void)hipFree(c->d_defer);
+  if (c->d_yflags) (void)hipFree(c->d_yflags);
   if (c->d_ndefer) (void)hipFree(c->d_ndefer);
   if (c->d_scene) (void)hipFree(c->d_scene);
   if (c->d_xtab) (void)hipFree(c->d_xtab);
@@ -350,6 +402,9 @@ static int launch_tile(lt_ctx* c, const lt_params* prm, const lt_tile_in* in,
                        const lt_tile_out* out, int Y, hipStream_t stream, hipStream_t rstream,
                        int set) {
   int64_t* dl = c->d_defer + (size_t)set * 2 * c->defer_cap;
+  // the spike / vertex planes go through per-pixel year flags ([2][n_pix] of this set)
+  uint64_t* yf = (out->spike || out->vertex) ? c->d_yflags + (size_t)set * 2 * c->defer_cap
+                                             : nullptr;
   unsigned long long* dn = c->d_ndefer + 4 * set;
   // [0]/[2]: deferred-pixel counts of the binary32 / binary64 lists (stage 1), [1]/[3]: the
   // resolve launches' work counters
@@ -375,10 +430,10 @@ static int launch_tile(lt_ctx* c, const lt_params* prm, const lt_tile_in* in,
   do {                                                                                     \
     if (i16)                                                                               \
       hipLaunchKernelGGL((analyze_fast_kernel<MY, RM, int16_t>), fgrid, fblock, 0, stream,   \
-                         c->d_scene, *prm, *in, *out, c->d_xtab, dl, dn);                  \
+                         c->d_scene, *prm, *in, *out, c->d_xtab, dl, dn, yf);              \
     else                                                                                   \
       hipLaunchKernelGGL((analyze_fast_kernel<MY, RM, float>), fgrid, fblock, 0, stream,     \
-                         c->d_scene, *prm, *in, *out, c->d_xtab, dl, dn);                  \
+                         c->d_scene, *prm, *in, *out, c->d_xtab, dl, dn, yf);              \
   } while (0)
 #ifdef LT_DEV_ONE_CONFIG  // A/B and assembly builds only: the (MAXY = LT_DEV_ONE_CONFIG, 1 rule)
   (void)one; (void)few;     // instances alone
@@ -406,7 +461,7 @@ static int launch_tile(lt_ctx* c, const lt_params* prm, const lt_tile_in* in,
     const unsigned g = resolve_grid<MY, RM, VT>(c->device);                                 \
     dim3 rg((unsigned)(nwave < (int64_t)g ? nwave : (int64_t)g));                           \
     hipLaunchKernelGGL((resolve_fast_kernel<MY, RM, VT>), rg, fblock, 0, stream, c->d_scene, \
-                       *prm, *in, *out, c->d_xtab, LIST, CNT);                              \
+                       *prm, *in, *out, c->d_xtab, LIST, CNT, yf);                          \
   } while (0)
 #define LT_LAUNCH_RESOLVE(MY, RM)                                                            \
   do {                                                                                      \
@@ -427,6 +482,18 @@ static int launch_tile(lt_ctx* c, const lt_params* prm, const lt_tile_in* in,
 #endif
 #undef LT_LAUNCH_RESOLVE
 #undef LT_LAUNCH_RESOLVE1
+  if (yf) {  // every pixel's flags are in (analyze + resolve): expand them into the planes
+    const bool v4 = ((uintptr_t)out->spike % 4 == 0) && ((uintptr_t)out->vertex % 4 == 0) &&
+                    out->stride % 4 == 0;
+    const int64_t nthr = v4 ? (in->n_pix + 3) / 4 : in->n_pix;
+    dim3 eg((unsigned)((nthr + kBlock - 1) / kBlock)), eb(kBlock);
+    if (v4)
+      hipLaunchKernelGGL((year_flags_kernel<true>), eg, eb, 0, stream, yf, in->n_pix, Y,
+                         out->spike, out->vertex, out->stride);
+    else
+      hipLaunchKernelGGL((year_flags_kernel<false>), eg, eb, 0, stream, yf, in->n_pix, Y,
+                         out->spike, out->vertex, out->stride);
+  }
   HIP_OR_FAIL(c, hipGetLastError());
   if (ep[1]) HIP_OR_FAIL(c, hipEventRecord(ep[1]->stop, rstream));
   HIP_OR_FAIL(c, hipEventRecord(c->ev_resolved[set], rstream));
@@ -521,7 +588,10 @@ int lt_analyze_tiles_after(lt_ctx* c, const lt_scene* sc, const lt_params* prm, 
     if (c->side) HIP_OR_FAIL(c, hipStreamSynchronize(c->side));
     if (c->d_defer) HIP_OR_FAIL(c, hipFree(c->d_defer));
     c->d_defer = nullptr;
+    if (c->d_yflags) HIP_OR_FAIL(c, hipFree(c->d_yflags));
+    c->d_yflags = nullptr;
     HIP_OR_FAIL(c, hipMalloc((void**)&c->d_defer, 2 * 2 * sizeof(int64_t) * (size_t)cap));
+    HIP_OR_FAIL(c, hipMalloc((void**)&c->d_yflags, 2 * 2 * sizeof(uint64_t) * (size_t)cap));
     if (!c->d_ndefer)
       HIP_OR_FAIL(c, hipMalloc((void**)&c->d_ndefer, 2 * 4 * sizeof(unsigned long long)));
     c->defer_cap = cap;

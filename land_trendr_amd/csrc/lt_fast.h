@@ -126,7 +126,8 @@ struct NoProbe {
 template <int MAXY, int RMAX, bool EXACT, class VT, class Probe = NoProbe>
 __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const lt_tile_in& in,
                                    const lt_tile_out& out, const lsq_xf* __restrict__ xtab,
-                                   int64_t p, bool live, int lane, WaveLds<MAXY, VT, EXACT>& L,
+                                   uint64_t* __restrict__ yflags, int64_t p, bool live, int lane,
+                                   WaveLds<MAXY, VT, EXACT>& L,
                                    const Probe& probe = Probe()) {
   const int Y = S.n_years;
   const int64_t is = in.stride, os = out.stride;
@@ -879,6 +880,9 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
     double cm = 0.0, cb = 0.0;       // eqn of the current vertex (right eqn of the points)
     double nm = 0.0, nb = 0.0;       // lookahead: eqn of the segment from the next vertex
     bool have_n = false;
+    // spike / vertex flags by year slot: with yflags the u8 planes are written from them by
+    // year_flags_kernel (lt_abi.hip) in 256-byte rows instead of 64-byte pieces here
+    uint64_t spk = 0, vtx = 0;
     int t = 0, k = 0, q = 0;         // present index, non-spike index, vertex number
     for (int y = 0; y < Y; y++) {    // wave-uniform
       const bool pr = good && ((pres >> y) & 1);
@@ -941,13 +945,22 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
         if (out.fit_b) out.fit_b[o] = pr ? fbv : nan;
         if (out.right_m) out.right_m[o] = pr ? cm : nan;
         if (out.right_b) out.right_b[o] = pr ? cb : nan;
-        if (out.spike) out.spike[o] = sp ? 1 : 0;
-        if (out.vertex) out.vertex[o] = isv ? 1 : 0;
+        if (yflags) {
+          spk |= (uint64_t)sp << y;
+          vtx |= (uint64_t)isv << y;
+        } else {
+          if (out.spike) out.spike[o] = sp ? 1 : 0;
+          if (out.vertex) out.vertex[o] = isv ? 1 : 0;
+        }
       }
       if (pr) {
         if (!sp) k++;
         t++;
       }
+    }
+    if (emit && yflags) {
+      yflags[p] = spk;
+      yflags[in.n_pix + p] = vtx;
     }
   } else if constexpr (!EXACT && RMAX <= LT_CERT_RULES) {
     // ---- labels only, certified. The rules need the fitted values at the vertices, and only the
