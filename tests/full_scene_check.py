@@ -10,7 +10,9 @@ trendline planes — winner, val_raw, val_fit, fit_m, fit_b, right_m, right_b, s
 Prints one progress line per chunk and writes a JSON summary.
 
 Usage (GPU box): python tests/full_scene_check.py --config c2 --out gpurun_out/full_c2.json
-(--first/--last: re-analyse one pixel range of the scene, to split a long check over calls)
+(--first/--last: re-analyse one pixel range of the scene, to split a long check over calls;
+--labels-only: only the label rasters, as bench.py requests them for c2/c3, so the analyze kernel
+takes its certified labels-only path)
 """
 import argparse
 import json
@@ -44,11 +46,18 @@ def main():
     ap.add_argument('--first', type=int, default=0, help='first pixel the oracle re-analyses')
     ap.add_argument('--last', type=int, default=0, help='end of that range (0: the scene end)')
     ap.add_argument('--threads', type=int, default=0)
+    ap.add_argument('--labels-only', action='store_true',
+                    help="the bench's own fields (label rasters only, the analyze kernel's "
+                         "certified labels path) instead of adding val_fit / vertex")
     ap.add_argument('--out', default='')
     args = ap.parse_args()
     c = bench.CONFIGS[args.config]
     P = args.pixels or c['pixels']
-    fields = LABELS + (tuple(bench.TRENDLINE_FIELDS) if c['trendline'] else ('val_fit', 'vertex'))
+    if args.labels_only:
+        fields = LABELS + ('initial_val',)
+    else:
+        fields = LABELS + (tuple(bench.TRENDLINE_FIELDS) if c['trendline'] else
+                           ('val_fit', 'vertex'))
     t0 = time.time()
     eng = get_engine(0)
     m = Mosaic([P], 1 << 24, 1, 0, 'by_scene')
@@ -83,7 +92,8 @@ def main():
                 diff[f] += int((~same).sum())
         print('oracle %d/%d px, differing values so far %d, %.0f s' % (
             b, end, sum(diff.values()), time.time() - t0), flush=True)
-    res = {'config': args.config, 'pixels': P, 'checked': [args.first, end],
+    res = {'config': args.config, 'labels_only': args.labels_only, 'pixels': P,
+           'checked': [args.first, end],
            'tile_pixels': m.tile, 'seed': c['seed'],
            'input': 'int16 bands + index_eqn "B1 - B2" (bench.py rank 0 scene, runner path)',
            'fields': list(fields), 'differing_values': diff,
