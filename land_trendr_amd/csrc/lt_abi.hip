@@ -138,8 +138,8 @@ __global__ __launch_bounds__(kBlock) void year_flags_kernel(const uint64_t* __re
       }
       const int64_t o = (int64_t)y * os + p;
       if (np == 4) {
-        if (spike) *(uint32_t*)(spike + o) = a;
-        if (vertex) *(uint32_t*)(vertex + o) = b;
+        if (spike) __builtin_nontemporal_store(a, (uint32_t*)(spike + o));
+        if (vertex) __builtin_nontemporal_store(b, (uint32_t*)(vertex + o));
       } else {
         for (int i = 0; i < np; i++) {
           if (spike) spike[o + i] = (uint8_t)(a >> (8 * i));
@@ -156,6 +156,17 @@ __global__ __launch_bounds__(kBlock) void year_flags_kernel(const uint64_t* __re
       if (vertex) vertex[o] = (uint8_t)((vf >> y) & 1);
     }
   }
+}
+
+// the binary64 analyze instance (lazy DP on a binary64 LDS series) exists for up to 4 rules
+template <int MAXY, int RMAX>
+static void launch_analyze_wide(dim3 grid, dim3 block, hipStream_t stream, const lt::DevScene* S,
+                                const lt_params& P, const lt_tile_in& in, const lt_tile_out& out,
+                                const lt::lsq_xf* xtab, int64_t* defer,
+                                unsigned long long* n_defer, uint64_t* yflags) {
+  if constexpr (RMAX <= 4)
+    hipLaunchKernelGGL((analyze_fast_kernel<MAXY, RMAX, double>), grid, block, 0, stream, S, P,
+                       in, out, xtab, defer, n_defer, yflags);
 }
 
 // waves of resolve_fast_kernel<MAXY, RMAX, VT> the device holds at once
@@ -426,11 +437,18 @@ static int launch_tile(lt_ctx* c, const lt_params* prm, const lt_tile_in* in,
   dim3 fgrid((unsigned)nwave), fblock(64);
   const bool one = prm->n_rules <= 1, few = prm->n_rules <= 4;
   const bool i16 = in->obs_index && in->index_type == LT_T_I16;
+  // binary64 values (obs_val, or an f64 index raster) take the binary64 analyze instance (up to
+  // 4 rules): the lazy DP on a binary64 LDS series; otherwise every value binary32 cannot hold
+  // would send its pixel to the exact-OPT resolve stage (46 vs 1842 Mpx/s, profiles/float_index.py)
+  const bool wide = (!in->obs_index || in->index_type == LT_T_F64) && prm->n_rules <= 4;
 #define LT_LAUNCH_FAST(MY, RM)                                                                 \
   do {                                                                                     \
     if (i16)                                                                               \
       hipLaunchKernelGGL((analyze_fast_kernel<MY, RM, int16_t>), fgrid, fblock, 0, stream,   \
                          c->d_scene, *prm, *in, *out, c->d_xtab, dl, dn, yf);              \
+    else if (wide)                                                                         \
+      launch_analyze_wide<MY, RM>(fgrid, fblock, stream, c->d_scene, *prm, *in, *out,      \
+                                  c->d_xtab, dl, dn, yf);                                  \
     else                                                                                   \
       hipLaunchKernelGGL((analyze_fast_kernel<MY, RM, float>), fgrid, fblock, 0, stream,     \
                          c->d_scene, *prm, *in, *out, c->d_xtab, dl, dn, yf);              \
@@ -466,6 +484,7 @@ static int launch_tile(lt_ctx* c, const lt_params* prm, const lt_tile_in* in,
 #define LT_LAUNCH_RESOLVE(MY, RM)                                                            \
   do {                                                                                      \
     if (i16) LT_LAUNCH_RESOLVE1(MY, RM, int16_t, dl, dn);                                   \
+    else if (wide) LT_LAUNCH_RESOLVE1(MY, RM, double, dl, dn);                              \
     else LT_LAUNCH_RESOLVE1(MY, RM, float, dl, dn);                                         \
     LT_LAUNCH_RESOLVE1(MY, RM, double, dl + in->n_pix, dn + 2);                             \
   } while (0)

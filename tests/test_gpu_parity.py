@@ -451,3 +451,18 @@ def test_labels_only_launch_matches_oracle_and_full_launch(engine, ds):
             same = ((a.view(np.int64) == got.view(np.int64)) | (np.isnan(a) & np.isnan(got))
                     if a.dtype.kind == 'f' else a == got)
             assert same.all(), (name, what, f, int((~same).sum()))
+
+
+@pytest.mark.parametrize('name', golden_io.scene_names())
+def test_golden_scene_as_float32_index_raster(engine, name):
+    """Binary64 values take the binary64 analyze instance; a float32 index raster keeps the
+    binary32 one. Every golden scene whose values binary32 holds exactly, fed as float32, must give
+    the golden outputs too."""
+    g = golden_io.GoldenScene(name)
+    v32 = np.asarray(g.values, np.float64).astype(np.float32)
+    if not np.array_equal(v32.astype(np.float64), np.asarray(g.values, np.float64),
+                          equal_nan=True):
+        pytest.skip('values not exact in binary32')
+    out = _run(engine, g.scene, g.params, v32, g.valid)
+    bad = golden_io.compare(g, out)
+    assert not bad, '\n'.join(bad[:40])
