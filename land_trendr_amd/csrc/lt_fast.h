@@ -733,25 +733,31 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
       // the column minimum in any lane, the column is complete; a start priced past that point
       // lies above the bound, so tracking it changes no decision
       bool more = j >= 2;  // wave-uniform
-      if (more) {  // starts j-2 and j-3 from the register window
+      if (more) {  // starts j-2 and j-3 from the register window, one at a time: the bound of
+        // start j-2 already covers j-3, so a wave whose lanes all leave there skips j-3
         const bool two = j >= 3;
-        double va, ha, la, ba, vb = 0.0, hb = 0.0, lb = 0.0, bb = 0.0;
-        bool nb = false;
+        double va, ha, la, ba;
         add_xy(wx2, wy2);
         const bool na = price(j - 2, opt_jm2, tg_jm2, va, ha, la, ba);
-        if (two) {
-          add_xy(wx3, wy3);
-          nb = price(j - 3, opt_jm3, tg_jm3, vb, hb, lb, bb);
-        }
         double Hb = upper();
-        if (__ballot(la <= Hb || (two && lb <= Hb))) {  // else neither can change a decision
-          const int z = zero_tests(j - 2, two, na, nb, wx3, wy3);
+        if (__ballot(la <= Hb)) {  // else it can change no decision
+          const int z = zero_tests(j - 2, false, na, false, 0, 0.0);
           offer(j - 2, opt_jm2, tg_jm2, va, ha, la, z & 1);
-          if (two) offer(j - 3, opt_jm3, tg_jm3, vb, hb, lb, z & 2);
           Hb = upper();
         }
-        if (prune && !__ballot(col && !(ba > Hb || (two && bb > Hb)))) more = false;
-        more = more && two;
+        bool go = !prune || __ballot(col && !(ba > Hb));
+        if (two && go) {
+          double vb, hb, lb, bb;
+          add_xy(wx3, wy3);
+          const bool nb = price(j - 3, opt_jm3, tg_jm3, vb, hb, lb, bb);
+          if (__ballot(lb <= Hb)) {
+            const int z = zero_tests(j - 3, false, nb, false, 0, 0.0);
+            offer(j - 3, opt_jm3, tg_jm3, vb, hb, lb, z & 1);
+            Hb = upper();
+          }
+          go = !prune || __ballot(col && !(bb > Hb));
+        }
+        more = go && two;
       }
       for (int ii = j - 4; more && ii >= 0; ii -= 2) {  // the rest from LDS / private memory
         const int i = __builtin_amdgcn_readfirstlane(ii);  // wave-uniform start
