@@ -687,25 +687,6 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
         const double N1 = __builtin_fma(md, sxy, -((double)sx * sy));
         return kZero * syy < 0x1p-54 * c && sse_exact_zero(t1, D, N1);
       };
-      // the zero tests of starts a = i and b = i - 1 (b's point xb, yb is the last one added;
-      // a's sums are the current ones less that point, exact for the integer data tested):
-      // bit 0 for a, bit 1 for b
-      auto zero_tests = [&](int i, bool two, bool na, bool nb, int xb, double yb)
-                            __attribute__((always_inline)) {
-        int z = 0;
-        if (__ballot(na || (two && nb))) {
-          const int m = j - i + 1;
-          if (two) {
-            if (na && zero_test(m, Sx - xb, Sxx - xb * xb, Sy - yb,
-                                __builtin_fma(-(double)xb, yb, Sxy), __builtin_fma(-yb, yb, Syy)))
-              z |= 1;
-            if (nb && zero_test(m + 1, Sx, Sxx, Sy, Sxy, Syy)) z |= 2;
-          } else if (na && zero_test(m, Sx, Sxx, Sy, Sxy, Syy)) {
-            z |= 1;
-          }
-        }
-        return z;
-      };
       // a start of >= 3 points: a zero-residual start (v recomputed as the reference's
       // fl(c + OPTa[i])) or an interval candidate that starts a new base if it wins
       auto offer = [&](int i, double o, int tg, double v, double hi, double lo, bool zr) __attribute__((always_inline)) {
@@ -728,65 +709,41 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
         const double h = Hi < Ve ? Hi : Ve;
         return gh < h ? gh : h;
       };
-      // the other starts two at a time: two independent pricing chains per iteration and one
-      // exit test. Early exit (dp_start_bound): once no start below i can reach an upper bound on
-      // the column minimum in any lane, the column is complete; a start priced past that point
-      // lies above the bound, so tracking it changes no decision
+      // start i (>= 3 points, its point already in the sums): priced, offered to the trackers when
+      // its lower end reaches the column's current upper bound (else it can change no decision),
+      // its early-exit bound returned
+      auto one_start = [&](int i, double o, int tg) __attribute__((always_inline)) {
+        double v, hi, lo, bnd;
+        const bool nz = price(i, o, tg, v, hi, lo, bnd);
+        if (__ballot(lo <= upper())) {
+          bool zr = false;
+          if (__ballot(nz)) zr = nz && zero_test(j - i + 1, Sx, Sxx, Sy, Sxy, Syy);
+          offer(i, o, tg, v, hi, lo, zr);
+        }
+        return bnd;
+      };
+      // early exit (dp_start_bound): once no start below i can reach an upper bound on the column
+      // minimum in any lane, the column is complete; a start priced past that point lies above the
+      // bound, so tracking it changes no decision. The starts go one at a time, each with its own
+      // exit test (pricing two per exit test: 2115 vs 2231 Mpx/s on c2, profiles/r02_ab_dp)
+      auto leave = [&](double bnd) __attribute__((always_inline)) {
+        return prune && !__ballot(col && !(bnd > upper()));
+      };
       bool more = j >= 2;  // wave-uniform
-      if (more) {  // starts j-2 and j-3 from the register window, one at a time: the bound of
-        // start j-2 already covers j-3, so a wave whose lanes all leave there skips j-3
-        const bool two = j >= 3;
-        double va, ha, la, ba;
+      if (more) {  // starts j-2 and j-3 from the register window
         add_xy(wx2, wy2);
-        const bool na = price(j - 2, opt_jm2, tg_jm2, va, ha, la, ba);
-        double Hb = upper();
-        if (__ballot(la <= Hb)) {  // else it can change no decision
-          const int z = zero_tests(j - 2, false, na, false, 0, 0.0);
-          offer(j - 2, opt_jm2, tg_jm2, va, ha, la, z & 1);
-          Hb = upper();
-        }
-        bool go = !prune || __ballot(col && !(ba > Hb));
-        if (two && go) {
-          double vb, hb, lb, bb;
+        more = !leave(one_start(j - 2, opt_jm2, tg_jm2));
+        if (j >= 3 && more) {
           add_xy(wx3, wy3);
-          const bool nb = price(j - 3, opt_jm3, tg_jm3, vb, hb, lb, bb);
-          if (__ballot(lb <= Hb)) {
-            const int z = zero_tests(j - 3, false, nb, false, 0, 0.0);
-            offer(j - 3, opt_jm3, tg_jm3, vb, hb, lb, z & 1);
-            Hb = upper();
-          }
-          go = !prune || __ballot(col && !(bb > Hb));
+          more = !leave(one_start(j - 3, opt_jm3, tg_jm3));
         }
-        more = go && two;
+        more = more && j >= 3;
       }
-      for (int ii = j - 4; more && ii >= 0; ii -= 2) {  // the rest from LDS / private memory
+      for (int ii = j - 4; more && ii >= 0; ii--) {  // the rest from LDS / private memory
         const int i = __builtin_amdgcn_readfirstlane(ii);  // wave-uniform start
-        const bool two = i >= 1;                            // wave-uniform
         add_xy(L.xn[i][lane], (double)L.ys[i][lane]);
-        double va, ha, la, ba, vb = 0.0, hb = 0.0, lb = 0.0, bb = 0.0;
-        bool nb = false;
-        const double oa = OPTa[i];
-        const int ta = ((exact >> i) & 1) ? 0 : -1;  // tags are kept in the window only
-        const bool na = price(i, oa, ta, va, ha, la, ba);
-        double ob = 0.0;
-        int tb = 0, xb = 0;
-        double yb = 0.0;
-        if (two) {
-          xb = L.xn[i - 1][lane];
-          yb = (double)L.ys[i - 1][lane];
-          add_xy(xb, yb);
-          ob = OPTa[i - 1];
-          tb = ((exact >> (i - 1)) & 1) ? 0 : -1;
-          nb = price(i - 1, ob, tb, vb, hb, lb, bb);
-        }
-        double Hb = upper();
-        if (__ballot(la <= Hb || (two && lb <= Hb))) {
-          const int z = zero_tests(i, two, na, nb, xb, yb);
-          offer(i, oa, ta, va, ha, la, z & 1);
-          if (two) offer(i - 1, ob, tb, vb, hb, lb, z & 2);
-          Hb = upper();
-        }
-        if (prune && !__ballot(col && !(ba > Hb || (two && bb > Hb)))) break;
+        // tags are kept in the window only: a start from private memory is exact or not
+        if (leave(one_start(i, OPTa[i], ((exact >> i) & 1) ? 0 : -1))) break;
       }
       // the group's best enters the trackers (an empty group: gv = inf, no effect)
       {
