@@ -10,9 +10,13 @@ generated in HBM before the timed region.
 A step = one pass of the hot path over the job (land_trendr_amd/runner.py, the code path the job
 runner uses too): per tile, the index_eqn load kernel (B1 - B2) on the load stream, analyze +
 label, then the tile's label rasters sent point-to-point to rank 0 over RCCL (N > 1), travelling
-while the next tile computes. After the timed steps: the load kernel timed alone (its HBM
+while the next tile computes. After the timed steps: the correctness gate (a seeded sample of
+every rank's pixels re-analysed by the CPU oracle and compared with every plane the timed steps
+wrote; any difference fails the run, exit status 3), the load kernel timed alone (its HBM
 roofline) and, unless --e2e-steps 0, end-to-end steps that add H2D of the pinned int16 bands and
 D2H of the label rasters (and, for c5, of every per-year trendline plane) to the same pipeline.
+The oracle (oracle/, test infrastructure) is only the checker and the CPU baseline here: it never
+produces a measured output.
 """
 import argparse
 import json
@@ -148,6 +152,48 @@ def cpu_baseline(cfg, seconds):
                       % (sample, threads, dt)}
 
 
+def parity_sample(runner, params, n_sample, threads, seed=12345):
+    """The oracle leg's correctness gate: a seeded sample of this rank's pixels,
+    re-analysed by the oracle (oracle/lt_oracle.c, the CPU checker) from the same index rasters
+    the timed steps read, against every output plane the timed steps wrote for them (labels only
+    where the rule matched: elsewhere both sides hold NODATA placeholders). Returns (pixels,
+    mismatching values, {field: mismatches})."""
+    import numpy as np
+    from oracle import oracle
+    items = runner.items
+    sizes = np.array([it.tile.n for it in items], np.int64)
+    if sizes.sum() == 0:
+        return 0, 0, {}
+    rng = np.random.default_rng(seed + runner.m.rank)
+    n = int(min(n_sample, sizes.sum()))
+    flat = np.sort(rng.choice(int(sizes.sum()), n, replace=False))
+    starts = np.concatenate([[0], np.cumsum(sizes)[:-1]])
+    tile_of = np.searchsorted(starts, flat, side='right') - 1
+    bad, per_field, checked = 0, {}, 0
+    for k in np.unique(tile_of):
+        it = items[k]
+        cols = torch.from_numpy(flat[tile_of == k] - starts[k]).to(it.values.device)
+        vals = it.values[:, cols].double().cpu().numpy()
+        valid = None if it.valid is None else it.valid[:, cols].cpu().numpy()
+        exp = oracle.analyze_tile(it.scene, params, vals, valid, n_threads=threads)
+        m = exp['matched'].astype(bool)
+        for f, plane in runner.outs[k].items():
+            got = plane[..., cols].cpu().numpy()
+            e = exp[f][:got.shape[0]] if got.ndim == 2 else exp[f]
+            if f in ('class_val', 'onset_year', 'duration', 'magnitude', 'initial_val'):
+                got, e = np.where(m[:got.shape[0]], got, 0), np.where(m[:got.shape[0]], e, 0)
+            if got.dtype.kind == 'f':
+                same = (got.view(np.int64) == e.view(np.int64)) | (np.isnan(got) & np.isnan(e))
+            else:
+                same = got == e
+            nb = int((~same).sum())
+            if nb:
+                per_field[f] = per_field.get(f, 0) + nb
+                bad += nb
+        checked += len(cols)
+    return checked, bad, per_field
+
+
 class _PinnedBands:
     """stage_in for MosaicRunner.step: tile k's int16 bands H2D from pinned host memory into
     device slab k % 2 on a copy stream, once the load kernel of tile k - 2 has read that slab."""
@@ -232,6 +278,9 @@ def main():
     ap.add_argument('--no-trendline', action='store_true',
                     help='attribution runs only: leave out the per-year trendline planes of a '
                          'trendline config (c5)')
+    ap.add_argument('--parity-sample', type=int, default=16384,
+                    help='pixels per rank re-analysed by the oracle after the timed steps and '
+                         'compared with every plane they wrote (0: skip; A/B timing runs only)')
     ap.add_argument('--serial-load', action='store_true',
                     help='run the index_eqn kernels on the analyze stream (no load stream)')
     args = ap.parse_args()
@@ -302,9 +351,24 @@ def main():
     elapsed = float(elapsed.item())
     index_ms = runner.index_ms()
 
-    # correctness gate on this run's own outputs: no pixel may be flagged as an unemulated path
+    # correctness gate on this run's own outputs: no pixel may be flagged as an unemulated path,
+    # and a seeded sample of the pixels must match the oracle in every plane the steps wrote
     n_numeric = sum(int(((o['status'][:it.tile.n] & 16) != 0).sum().item())
                     for o, it in zip(runner.outs, items))
+    psample = None
+    if args.parity_sample > 0:
+        avail, quota = host_cores()
+        thr = avail if quota is None else max(1, min(avail, int(math.ceil(quota))))
+        t_ps = time.perf_counter()
+        checked, bad, per_field = parity_sample(runner, params, args.parity_sample, thr)
+        res_t = torch.tensor([checked, bad], dtype=torch.float64, device=dev)
+        if dist is not None:
+            dist.all_reduce(res_t)
+        psample = {'pixels': int(res_t[0].item()), 'mismatched_values': int(res_t[1].item()),
+                   'fields': sorted(runner.fields), 'mismatches_rank0': per_field,
+                   'seconds_rank0': round(time.perf_counter() - t_ps, 2),
+                   'checker': 'oracle/lt_oracle.c on a seeded sample of each rank\'s pixels, '
+                              'from the index rasters the timed steps read'}
     # the load kernel alone (its HBM roofline): one tile, serially, after the timed region
     it0 = items[0]
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
@@ -413,6 +477,7 @@ def main():
                      # kernel proves most candidate fits irrelevant and never computes them)
                      'reference_work_equivalent_tflops': round(ref_equiv, 2)},
         'status_numeric_pixels': n_numeric,
+        'parity_sample': psample,
         'load_stage': {
             'kernel': 'lt_index_kernel4 (hiprtc, index_eqn "B1 - B2", int16 bands -> int16)',
             'ms_per_launch_overlapped': r(index_ms, 3),
@@ -433,6 +498,10 @@ def main():
         print(json.dumps(res), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+    if psample is not None and psample['mismatched_values'] != 0:
+        print('bench: %d values of the parity sample differ from the oracle'
+              % psample['mismatched_values'], file=sys.stderr)
+        sys.exit(3)
 
 
 if __name__ == '__main__':

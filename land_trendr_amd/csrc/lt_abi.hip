@@ -12,7 +12,7 @@
 #include <vector>
 
 #include "../../include/lt_abi.h"
-#include "lt_fast.h"
+#include "lt_launch.h"
 #include "lt_pixel.h"
 #include "lt_index.h"
 #include "lt_settings.h"
@@ -21,80 +21,6 @@
 namespace {
 
 constexpr int kBlock = 256;
-
-__device__ inline void defer_append(bool deferred, int64_t p, int lane, int64_t* __restrict__ list,
-                                    unsigned long long* __restrict__ count) {
-  const uint64_t mask = __ballot(deferred);
-  if (mask == 0) return;
-  const int leader = __ffsll((long long)mask) - 1;
-  unsigned long long base = 0;
-  if (lane == leader) base = atomicAdd(count, (unsigned long long)__popcll(mask));
-  base = __shfl(base, leader);
-  if (deferred) list[base + __popcll(mask & ((1ull << lane) - 1))] = p;
-}
-
-// Stage 1 (wave-lockstep body, lt_fast.h): one wave per workgroup, the pixel series in LDS.
-// Occupancy target: 4 waves per SIMD (<= 128 VGPRs) where the body fits without spilling.
-#ifndef LT_FAST_WAVES_C2  // waves per SIMD the single-rule MAXY <= 32 instance is built for
-#define LT_FAST_WAVES_C2 4
-#endif
-#ifndef LT_FAST_WAVES_BIG
-#define LT_FAST_WAVES_BIG 4
-#endif
-// the analyze stage's phase probe: lt::NoProbe (nothing) except in the profiling build
-// (profiles/stamps.sh defines it as the cycle-stamping probe of profiles/stamp_probe.h)
-#ifndef LT_ANALYZE_PROBE
-#define LT_ANALYZE_PROBE lt::NoProbe
-#endif
-// VT: the LDS type of the series — int16 when the tile's index raster is int16 (every value fits;
-// half the LDS of binary32, so more waves per CU), else binary32 (values it cannot hold defer the
-// pixel to the binary64 resolve).
-template <int MAXY, int RMAX, class VT>
-__global__ __launch_bounds__(64, (MAXY <= 32 && RMAX == 1) ? LT_FAST_WAVES_C2 : LT_FAST_WAVES_BIG) void analyze_fast_kernel(const lt::DevScene* __restrict__ S,
-                                                          const lt_params P, const lt_tile_in in,
-                                                          const lt_tile_out out,
-                                                          const lt::lsq_xf* __restrict__ xtab,
-                                                          int64_t* __restrict__ defer,
-                                                          unsigned long long* __restrict__ n_defer,
-                                                          uint64_t* __restrict__ yflags) {
-  __shared__ lt::WaveLds<MAXY, VT, false> L;
-  const int lane = threadIdx.x;
-  const int64_t p = (int64_t)blockIdx.x * 64 + lane;
-  const bool live = p < in.n_pix;
-  const int d = lt::analyze_fast<MAXY, RMAX, false, VT>(*S, P, in, out, xtab, yflags, p, live,
-                                                        lane, L, LT_ANALYZE_PROBE{});
-  // two lists: [0, n_pix) for the binary32 resolve, [n_pix, 2 n_pix) for the binary64 one;
-  // counters [0] / [2] count them (wave-aggregated atomics)
-  defer_append(live && d == lt::kDeferExact, p, lane, defer, &n_defer[0]);
-  defer_append(live && d == lt::kDeferWide, p, lane, defer + in.n_pix, &n_defer[2]);
-}
-
-// Stage 2 (wave-lockstep, lt_fast.h with EXACT): the deferred pixels, binary64 series in LDS,
-// exact-OPT DP. A grid of exactly the resident waves takes 64-pixel groups of the list from a
-// counter (group cost varies a lot); every wave leaves once the counter has passed the list.
-template <int MAXY, int RMAX, class VT>
-__global__ __launch_bounds__(64) void resolve_fast_kernel(const lt::DevScene* __restrict__ S,
-                                                          const lt_params P, const lt_tile_in in,
-                                                          const lt_tile_out out,
-                                                          const lt::lsq_xf* __restrict__ xtab,
-                                                          const int64_t* __restrict__ defer,
-                                                          unsigned long long* __restrict__ counters,
-                                                          uint64_t* __restrict__ yflags) {
-  __shared__ lt::WaveLds<MAXY, VT, true> L;
-  const int lane = threadIdx.x;
-  const int64_t n = (int64_t)counters[0];  // written by stage 1, a previous launch
-  for (;;) {
-    unsigned g = 0;
-    if (lane == 0) g = atomicAdd((unsigned*)&counters[1], 1u);
-    g = __builtin_amdgcn_readfirstlane(__shfl(g, 0));
-    const int64_t base = (int64_t)g * 64;
-    if (base >= n) break;
-    const int64_t k = base + lane;
-    const bool live = k < n;
-    lt::analyze_fast<MAXY, RMAX, true, VT>(*S, P, in, out, xtab, yflags, live ? defer[k] : 0,
-                                           live, lane, L);
-  }
-}
 
 // one lsq_factor per slot of the x-set table (lt_lapack.h), computed by the device arithmetic
 // that the lookups replace
@@ -156,36 +82,6 @@ __global__ __launch_bounds__(kBlock) void year_flags_kernel(const uint64_t* __re
       if (vertex) vertex[o] = (uint8_t)((vf >> y) & 1);
     }
   }
-}
-
-// the binary64 analyze instance (lazy DP on a binary64 LDS series) exists for up to 4 rules
-template <int MAXY, int RMAX>
-static void launch_analyze_wide(dim3 grid, dim3 block, hipStream_t stream, const lt::DevScene* S,
-                                const lt_params& P, const lt_tile_in& in, const lt_tile_out& out,
-                                const lt::lsq_xf* xtab, int64_t* defer,
-                                unsigned long long* n_defer, uint64_t* yflags) {
-  if constexpr (RMAX <= 4)
-    hipLaunchKernelGGL((analyze_fast_kernel<MAXY, RMAX, double>), grid, block, 0, stream, S, P,
-                       in, out, xtab, defer, n_defer, yflags);
-}
-
-// waves of resolve_fast_kernel<MAXY, RMAX, VT> the device holds at once
-template <int MAXY, int RMAX, class VT>
-static unsigned resolve_grid(int device) {
-  static int cached_dev = -1;
-  static unsigned cached = 0;
-  if (cached_dev != device) {
-    int per_cu = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, resolve_fast_kernel<MAXY, RMAX, VT>,
-                                                     64, 0) != hipSuccess || per_cu < 1)
-      per_cu = 1;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
-        cus < 1)
-      cus = 256;
-    cached = (unsigned)(per_cu * cus);
-    cached_dev = device;
-  }
-  return cached;
 }
 
 struct YearArg {
@@ -434,39 +330,8 @@ static int launch_tile(lt_ctx* c, const lt_params* prm, const lt_tile_in* in,
   if (ep[0]) HIP_OR_FAIL(c, hipEventRecord(ep[0]->start, stream));
   const int64_t nwave = (in->n_pix + 63) / 64;
   if (nwave > 0x7fffffff) return fail(c, LT_ERR_LIMIT, "tile too large%s");
-  dim3 fgrid((unsigned)nwave), fblock(64);
-  const bool one = prm->n_rules <= 1, few = prm->n_rules <= 4;
-  const bool i16 = in->obs_index && in->index_type == LT_T_I16;
-  // binary64 values (obs_val, or an f64 index raster) take the binary64 analyze instance (up to
-  // 4 rules): the lazy DP on a binary64 LDS series; otherwise every value binary32 cannot hold
-  // would send its pixel to the exact-OPT resolve stage (46 vs 1842 Mpx/s, profiles/float_index.py)
-  const bool wide = (!in->obs_index || in->index_type == LT_T_F64) && prm->n_rules <= 4;
-#define LT_LAUNCH_FAST(MY, RM)                                                                 \
-  do {                                                                                     \
-    if (i16)                                                                               \
-      hipLaunchKernelGGL((analyze_fast_kernel<MY, RM, int16_t>), fgrid, fblock, 0, stream,   \
-                         c->d_scene, *prm, *in, *out, c->d_xtab, dl, dn, yf);              \
-    else if (wide)                                                                         \
-      launch_analyze_wide<MY, RM>(fgrid, fblock, stream, c->d_scene, *prm, *in, *out,      \
-                                  c->d_xtab, dl, dn, yf);                                  \
-    else                                                                                   \
-      hipLaunchKernelGGL((analyze_fast_kernel<MY, RM, float>), fgrid, fblock, 0, stream,     \
-                         c->d_scene, *prm, *in, *out, c->d_xtab, dl, dn, yf);              \
-  } while (0)
-#ifdef LT_DEV_ONE_CONFIG  // A/B and assembly builds only: the (MAXY = LT_DEV_ONE_CONFIG, 1 rule)
-  (void)one; (void)few;     // instances alone
-  LT_LAUNCH_FAST(LT_DEV_ONE_CONFIG, 1);
-#else
-  if (Y <= 32) {
-    if (one) LT_LAUNCH_FAST(32, 1); else if (few) LT_LAUNCH_FAST(32, 4); else LT_LAUNCH_FAST(32, 16);
-  } else if (Y <= 48) {
-    if (one) LT_LAUNCH_FAST(48, 1); else if (few) LT_LAUNCH_FAST(48, 4); else LT_LAUNCH_FAST(48, 16);
-  } else {
-    if (one) LT_LAUNCH_FAST(64, 1); else if (few) LT_LAUNCH_FAST(64, 4); else LT_LAUNCH_FAST(64, 16);
-  }
-#endif
-#undef LT_LAUNCH_FAST
-  HIP_OR_FAIL(c, hipGetLastError());
+  lt::TileLaunch l{c->d_scene, prm, in, out, c->d_xtab, dl, dn, yf, Y, c->device, stream};
+  HIP_OR_FAIL(c, lt::launch_analyze(l));
   if (ep[0]) HIP_OR_FAIL(c, hipEventRecord(ep[0]->stop, stream));
   if (rstream != stream) {
     HIP_OR_FAIL(c, hipEventRecord(c->ev_analyzed[set], stream));
@@ -474,33 +339,8 @@ static int launch_tile(lt_ctx* c, const lt_params* prm, const lt_tile_in* in,
   }
   if (ep[1]) HIP_OR_FAIL(c, hipEventRecord(ep[1]->start, rstream));
   stream = rstream;  // the resolve launches below
-#define LT_LAUNCH_RESOLVE1(MY, RM, VT, LIST, CNT)                                            \
-  do {                                                                                      \
-    const unsigned g = resolve_grid<MY, RM, VT>(c->device);                                 \
-    dim3 rg((unsigned)(nwave < (int64_t)g ? nwave : (int64_t)g));                           \
-    hipLaunchKernelGGL((resolve_fast_kernel<MY, RM, VT>), rg, fblock, 0, stream, c->d_scene, \
-                       *prm, *in, *out, c->d_xtab, LIST, CNT, yf);                          \
-  } while (0)
-#define LT_LAUNCH_RESOLVE(MY, RM)                                                            \
-  do {                                                                                      \
-    if (i16) LT_LAUNCH_RESOLVE1(MY, RM, int16_t, dl, dn);                                   \
-    else if (wide) LT_LAUNCH_RESOLVE1(MY, RM, double, dl, dn);                              \
-    else LT_LAUNCH_RESOLVE1(MY, RM, float, dl, dn);                                         \
-    LT_LAUNCH_RESOLVE1(MY, RM, double, dl + in->n_pix, dn + 2);                             \
-  } while (0)
-#ifdef LT_DEV_ONE_CONFIG
-  LT_LAUNCH_RESOLVE(LT_DEV_ONE_CONFIG, 1);
-#else
-  if (Y <= 32) {
-    if (one) LT_LAUNCH_RESOLVE(32, 1); else if (few) LT_LAUNCH_RESOLVE(32, 4); else LT_LAUNCH_RESOLVE(32, 16);
-  } else if (Y <= 48) {
-    if (one) LT_LAUNCH_RESOLVE(48, 1); else if (few) LT_LAUNCH_RESOLVE(48, 4); else LT_LAUNCH_RESOLVE(48, 16);
-  } else {
-    if (one) LT_LAUNCH_RESOLVE(64, 1); else if (few) LT_LAUNCH_RESOLVE(64, 4); else LT_LAUNCH_RESOLVE(64, 16);
-  }
-#endif
-#undef LT_LAUNCH_RESOLVE
-#undef LT_LAUNCH_RESOLVE1
+  l.stream = rstream;
+  HIP_OR_FAIL(c, lt::launch_resolve(l));
   if (yf) {  // every pixel's flags are in (analyze + resolve): expand them into the planes
     const bool v4 = ((uintptr_t)out->spike % 4 == 0) && ((uintptr_t)out->vertex % 4 == 0) &&
                     out->stride % 4 == 0;
@@ -571,7 +411,7 @@ int lt_analyze_tiles_after(lt_ctx* c, const lt_scene* sc, const lt_params* prm, 
   tmp.n_years = Y;
   for (int y = 0; y < Y; y++) {
     tmp.year[y] = sc->year[y];
-    tmp.feb29_bad[y] = sc->feb29_bad ? sc->feb29_bad[y] : 0;
+    if (sc->feb29_bad && sc->feb29_bad[y]) tmp.feb29_mask |= 1ull << y;
   }
   for (int y = 0; y <= Y; y++) tmp.slot_begin[y] = Y > 0 ? sc->slot_begin[y] : 0;
   for (int k = 0; k < K; k++) {

@@ -2,14 +2,16 @@
 // workgroup). Same results as analyze_pixel<.., true> in lt_pixel.h, organised for CDNA4:
 //
 //   * per-lane series live in LDS as [index][lane] planes: lane l of element k is at
-//     base + (k*64 + l) * sizeof(T), so any per-lane index k is bank-conflict free
-//     (ds_read_b64: bank = (2l) mod 64 within each 32-lane group);
+//     base + (k*64 + l) * sizeof(T), so lanes reading one index k touch consecutive words;
+//     lanes at different indices (a per-lane k) can still meet in a bank (PMC: 0.77 conflict
+//     cycles per LDS instruction on c2, 0.96 on c3 — small next to ~520 LDS instructions a wave);
 //   * loops run over a wave-uniform counter (series position, DP column, vertex number, rule)
 //     with per-lane predicates, so the expensive calls (LAPACK-emulated vertex fits) are issued
 //     once per vertex NUMBER for the whole wave instead of once per series position per lane;
 //   * the DP keeps OPT in registers (static indices from the unrolled inner loop) and decides a
 //     column without LAPACK emulation whenever the closed-form prices separate (dp_lazy's rule);
-//   * no scratch memory.
+//   * scratch: the analyze stage's OPT values of the DP (OPTa, read at wave-uniform indices
+//     below the four-column register window) and a few spills live in per-lane private memory.
 #pragma once
 #include <type_traits>
 
@@ -200,7 +202,7 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
       const int64_t q = (int64_t)y * os + p;
       if (out.winner) __builtin_nontemporal_store((int16_t)best[u], out.winner + q);
       if (best[u] >= 0) {
-        if (S.feb29_bad[y]) status |= LT_ST_FEB29;
+        if ((S.feb29_mask >> y) & 1) status |= LT_ST_FEB29;
         const double v = val[u];
         if (T == 0) y0 = S.year[y];
         const VT vs = (VT)v;

@@ -1,0 +1,153 @@
+// lt_kernels.h — the analyze and resolve kernels around the wave-lockstep body of lt_fast.h, and
+// the launch of one (MAXY, RMAX) instance pair. Included by the dispatch translation units only
+// (lt_dispatch.hip: every instance the product needs; the profiling units of profiles/: one
+// instance with a phase probe).
+//
+// Replaces, per pixel tile, the per-grid-point loop of MRLandTrendrJob.analysis_reducer
+// (/root/reference/mr_land_trendr_job.py:83-126) around utils.analyze + utils.change_labeling.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "lt_fast.h"
+#include "lt_launch.h"
+
+namespace lt {
+
+__device__ inline void defer_append(bool deferred, int64_t p, int lane, int64_t* __restrict__ list,
+                                    unsigned long long* __restrict__ count) {
+  const uint64_t mask = __ballot(deferred);
+  if (mask == 0) return;
+  const int leader = __ffsll((long long)mask) - 1;
+  unsigned long long base = 0;
+  if (lane == leader) base = atomicAdd(count, (unsigned long long)__popcll(mask));
+  base = __shfl(base, leader);
+  if (deferred) list[base + __popcll(mask & ((1ull << lane) - 1))] = p;
+}
+
+// Stage 1 (wave-lockstep body, lt_fast.h): one wave per workgroup, the pixel series in LDS.
+// WAVES: the waves per SIMD the instance is built for (<= 128 VGPRs at 4). VT: the LDS type of
+// the series — int16 when the tile's index raster is int16 (every value fits; half the LDS of
+// binary32, so more waves per CU), binary64 for binary64 values, else binary32 (values it cannot
+// hold defer the pixel to the binary64 resolve). Probe: lt_fast.h's phase probe (NoProbe here;
+// the profiling units of profiles/ pass theirs).
+template <int MAXY, int RMAX, class VT, int WAVES, class Probe>
+__global__ __launch_bounds__(64, WAVES) void analyze_fast_kernel(
+    const DevScene* __restrict__ S, const lt_params P, const lt_tile_in in, const lt_tile_out out,
+    const lsq_xf* __restrict__ xtab, int64_t* __restrict__ defer,
+    unsigned long long* __restrict__ n_defer, uint64_t* __restrict__ yflags) {
+  __shared__ WaveLds<MAXY, VT, false> L;
+  const int lane = threadIdx.x;
+  const int64_t p = (int64_t)blockIdx.x * 64 + lane;
+  const bool live = p < in.n_pix;
+  const int d = analyze_fast<MAXY, RMAX, false, VT>(*S, P, in, out, xtab, yflags, p, live, lane, L,
+                                                    Probe{});
+  // two lists: [0, n_pix) for the binary32 resolve, [n_pix, 2 n_pix) for the binary64 one;
+  // counters [0] / [2] count them (wave-aggregated atomics)
+  defer_append(live && d == kDeferExact, p, lane, defer, &n_defer[0]);
+  defer_append(live && d == kDeferWide, p, lane, defer + in.n_pix, &n_defer[2]);
+}
+
+// Stage 2 (wave-lockstep, lt_fast.h with EXACT): the deferred pixels, binary64 series in LDS,
+// exact-OPT DP. A grid of exactly the resident waves takes 64-pixel groups of the list from a
+// counter (group cost varies a lot); every wave leaves once the counter has passed the list.
+template <int MAXY, int RMAX, class VT>
+__global__ __launch_bounds__(64) void resolve_fast_kernel(const DevScene* __restrict__ S,
+                                                          const lt_params P, const lt_tile_in in,
+                                                          const lt_tile_out out,
+                                                          const lsq_xf* __restrict__ xtab,
+                                                          const int64_t* __restrict__ defer,
+                                                          unsigned long long* __restrict__ counters,
+                                                          uint64_t* __restrict__ yflags) {
+  __shared__ WaveLds<MAXY, VT, true> L;
+  const int lane = threadIdx.x;
+  const int64_t n = (int64_t)counters[0];  // written by stage 1, a previous launch
+  for (;;) {
+    unsigned g = 0;
+    if (lane == 0) g = atomicAdd((unsigned*)&counters[1], 1u);
+    g = __builtin_amdgcn_readfirstlane(__shfl(g, 0));
+    const int64_t base = (int64_t)g * 64;
+    if (base >= n) break;
+    const int64_t k = base + lane;
+    const bool live = k < n;
+    analyze_fast<MAXY, RMAX, true, VT>(*S, P, in, out, xtab, yflags, live ? defer[k] : 0, live,
+                                       lane, L);
+  }
+}
+
+// waves of resolve_fast_kernel<MAXY, RMAX, VT> the device holds at once
+template <int MAXY, int RMAX, class VT>
+inline unsigned resolve_grid(int device) {
+  static int cached_dev = -1;
+  static unsigned cached = 0;
+  if (cached_dev != device) {
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, resolve_fast_kernel<MAXY, RMAX, VT>,
+                                                     64, 0) != hipSuccess || per_cu < 1)
+      per_cu = 1;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
+        cus < 1)
+      cus = 256;
+    cached = (unsigned)(per_cu * cus);
+    cached_dev = device;
+  }
+  return cached;
+}
+
+// the tile's series type: int16 for an int16 index raster; binary64 for binary64 values (obs_val
+// or an f64 index raster) with up to 4 rules — the lazy DP on a binary64 LDS series, where
+// otherwise every value binary32 cannot hold would send its pixel to the exact-OPT resolve stage
+// (46 vs 1842 Mpx/s, profiles/float_index.py); else binary32
+enum SeriesKind { kSeriesI16, kSeriesF64, kSeriesF32 };
+inline SeriesKind series_kind(const TileLaunch& l) {
+  if (l.in->obs_index && l.in->index_type == LT_T_I16) return kSeriesI16;
+  if ((!l.in->obs_index || l.in->index_type == LT_T_F64) && l.params->n_rules <= 4)
+    return kSeriesF64;
+  return kSeriesF32;
+}
+
+inline dim3 tile_grid(const TileLaunch& l) { return dim3((unsigned)((l.in->n_pix + 63) / 64)); }
+
+template <int MAXY, int RMAX, int WAVES, class Probe>
+hipError_t launch_analyze_instance(const TileLaunch& l) {
+  const dim3 grid = tile_grid(l), block(64);
+  const SeriesKind k = series_kind(l);
+  if (k == kSeriesI16) {
+    hipLaunchKernelGGL((analyze_fast_kernel<MAXY, RMAX, int16_t, WAVES, Probe>), grid, block, 0,
+                       l.stream, l.scene, *l.params, *l.in, *l.out, l.xtab, l.defer, l.counters,
+                       l.yflags);
+  } else if (k == kSeriesF64) {
+    if constexpr (RMAX <= 4)  // the binary64 analyze instance exists for up to 4 rules
+      hipLaunchKernelGGL((analyze_fast_kernel<MAXY, RMAX, double, WAVES, Probe>), grid, block, 0,
+                         l.stream, l.scene, *l.params, *l.in, *l.out, l.xtab, l.defer, l.counters,
+                         l.yflags);
+  } else {
+    hipLaunchKernelGGL((analyze_fast_kernel<MAXY, RMAX, float, WAVES, Probe>), grid, block, 0,
+                       l.stream, l.scene, *l.params, *l.in, *l.out, l.xtab, l.defer, l.counters,
+                       l.yflags);
+  }
+  return hipGetLastError();
+}
+
+template <int MAXY, int RMAX, class VT>
+void launch_resolve1(const TileLaunch& l, const int64_t* list, unsigned long long* counters) {
+  const unsigned g = resolve_grid<MAXY, RMAX, VT>(l.device);
+  const int64_t nwave = (l.in->n_pix + 63) / 64;
+  const dim3 grid((unsigned)(nwave < (int64_t)g ? nwave : (int64_t)g)), block(64);
+  hipLaunchKernelGGL((resolve_fast_kernel<MAXY, RMAX, VT>), grid, block, 0, l.stream, l.scene,
+                     *l.params, *l.in, *l.out, l.xtab, list, counters, l.yflags);
+}
+
+// both deferred lists: the first in the tile's series type, the second (values binary32 cannot
+// hold) in binary64
+template <int MAXY, int RMAX>
+hipError_t launch_resolve_instance(const TileLaunch& l) {
+  const SeriesKind k = series_kind(l);
+  if (k == kSeriesI16) launch_resolve1<MAXY, RMAX, int16_t>(l, l.defer, l.counters);
+  else if (k == kSeriesF64) launch_resolve1<MAXY, RMAX, double>(l, l.defer, l.counters);
+  else launch_resolve1<MAXY, RMAX, float>(l, l.defer, l.counters);
+  launch_resolve1<MAXY, RMAX, double>(l, l.defer + l.in->n_pix, l.counters + 2);
+  return hipGetLastError();
+}
+
+}  // namespace lt

@@ -21,9 +21,11 @@ namespace lt {
 struct DevScene {
   int32_t n_obs;
   int32_t n_years;
+  // bit y: the target is Feb-29 and year y is not a leap year (one word: a scalar load, where a
+  // byte array needs a vector load — and on CDNA a vector load waits for every pending store)
+  uint64_t feb29_mask;
   int32_t year[LT_MAX_YEARS];
   int32_t slot_begin[LT_MAX_YEARS + 1];
-  uint8_t feb29_bad[LT_MAX_YEARS];
   int32_t order[LT_MAX_OBS];
   int32_t dist[LT_MAX_OBS];
   // pick_winners' winner per year slot when every observation is valid (no cloud mask): the same
@@ -531,7 +533,7 @@ __host__ __device__ bool analyze_pixel(const DevScene& S, const lt_params& P, co
     }
     if (out.winner) out.winner[(int64_t)y * os + p] = (int16_t)best;
     if (best >= 0) {
-      if (S.feb29_bad[y]) status |= LT_ST_FEB29;
+      if ((S.feb29_mask >> y) & 1) status |= LT_ST_FEB29;
       val[T] = obs_value(in, (int64_t)best * is + p);
       slot[T] = (uint8_t)y;
       T++;

@@ -523,6 +523,12 @@ struct EqnCompiler {
   std::string src;
   size_t p = 0;
   int depth = 0;  // parentheses (newlines allowed inside)
+  int nest = 0;   // recursion depth of atom '(' and unary signs: capped, so no input can
+                  // exhaust the native stack (the Python host's parser stops at 200 nested
+                  // parentheses; sign chains on a constant it folds until its own recursion
+                  // limit, on a band they exceed its 64 operations)
+  int signs = 0;
+  static constexpr int kMaxNest = 200, kMaxSigns = 500;
   std::vector<int> bands;
   NT band_t;
   std::vector<lt_index_op> ops;
@@ -692,7 +698,10 @@ struct EqnCompiler {
     if (c == '(') {
       p++;
       depth++;
+      if (++nest > kMaxNest)
+        throw Fail{LT_ERR_ARG, LT_EXC_VALUE, "index_eqn: too many nested parentheses"};
       Operand o = expr();
+      nest--;
       ws();
       if (p >= src.size() || src[p] != ')') syntax("')' expected");
       p++;
@@ -737,7 +746,11 @@ struct EqnCompiler {
     if (p < src.size() && (src[p] == '-' || src[p] == '+')) {
       const bool neg = src[p] == '-';
       p++;
+      // the host rejects long sign chains too (more than 64 operations, or none on a band)
+      if (++signs > kMaxSigns)
+        throw Fail{LT_ERR_ARG, LT_EXC_VALUE, "index_eqn: too many nested unary operators"};
       Operand v = unary();
+      signs--;
       if (!v.array) {
         if (neg) {
           if (v.s.is_float) v.s.f = -v.s.f;

@@ -186,8 +186,9 @@ class TrendlineStream:
 
     A tile's [Y, tile] planes are copied one row (one year plane, contiguous) at a time into the
     next ring buffer; a buffer is reused once its previous copy has completed (the host writer
-    reads it in between: `sink(field, row, host_view)` is called for each completed row when its
-    buffer comes round again, and for the rest by drain()). The copy stream waits for the work
+    reads it in between: `sink(field, row, host_view, key)` is called for each completed row when
+    its buffer comes round again, and for the rest by drain(); `key` is what push() was given,
+    e.g. the tile). The copy stream waits for the work
     queued on the current stream when push() is called, so queue tile t + 1's kernels before
     pushing tile t: its copies then overlap them, and a push that blocks on the ring does not
     hold back the next tile's launches."""
@@ -197,7 +198,7 @@ class TrendlineStream:
         self.stream = torch.cuda.Stream(self.device)
         self.ring = [torch.empty(int(row_bytes), dtype=torch.uint8, pin_memory=True)
                      for _ in range(depth)]
-        self.pending = [None] * depth  # (event, field, row, nbytes) of the buffer's last copy
+        self.pending = [None] * depth  # (event, field, row, nbytes, key) of the buffer's last copy
         self.sink = sink
         self.count = 0
         self.bytes = 0
@@ -206,13 +207,13 @@ class TrendlineStream:
         p = self.pending[slot]
         if p is None:
             return
-        ev, f, row, nb = p
+        ev, f, row, nb, key = p
         ev.synchronize()
         if self.sink is not None:
-            self.sink(f, row, self.ring[slot][:nb])
+            self.sink(f, row, self.ring[slot][:nb], key)
         self.pending[slot] = None
 
-    def push(self, planes, n=None):
+    def push(self, planes, n=None, key=None):
         """Queue the D2H of every row of planes[f] ([rows, W] device tensors; the first n pixels
         of each row, all W by default) after the work queued so far on the current stream."""
         ready = torch.cuda.Event()
@@ -233,7 +234,7 @@ class TrendlineStream:
                     dst.copy_(src.view(torch.uint8), non_blocking=True)
                     ev = torch.cuda.Event()
                     ev.record()
-                self.pending[slot] = (ev, f, r, nb)
+                self.pending[slot] = (ev, f, r, nb, key)
                 self.count += 1
                 self.bytes += nb
 

@@ -13,10 +13,15 @@ Steps, as the reference chains them:
   2. parse    (parse_mapper :47-81)   ingest.ingest_stack: band samples + mask validity per grid
                                       point (index_eqn runs on the GPU in step 3);
   3. analysis (analysis_reducer :83-126) the mosaic path of runner.py over pixel tiles on the GPU
-                                      (tiles round-robin over the torchrun ranks, every output
-                                      plane sent to rank 0);
+                                      (tiles round-robin over the torchrun ranks; the label planes
+                                      go to rank 0 over RCCL, the per-year trendline planes stream
+                                      to host memory per tile — a file-backed map shared by the
+                                      ranks when there are several — never to one GPU);
   4. output   (output_reducer :128-152) raster.label_rasters / trendline_rasters placed by each
                                       grid point's template offsets, written as GeoTIFFs.
+
+Multi-rank jobs: rank 0 alone extracts the compressed rasters and writes the grid, then every rank
+reads them (a barrier between), so no rank sees a partial extraction or a truncated grid.
 
 Errors follow the reference: a pixel the reference's analysis raises for fails the job with the
 same exception type (on_error='raise'); on_error='skip' leaves such pixels NODATA instead.
@@ -45,7 +50,9 @@ OUT_RASTS = '%s/output/rasters/'
 class LocalJob:
     def __init__(self, root, job, device=None, tile_pixels=1 << 22, trendline=True,
                  raster_mode='reference', pre_threshold_mode='reference', on_error='raise',
-                 work_dir=None):
+                 work_dir=None, engine=None):
+        """engine: the analysis engine (default: engine.get_engine of `device`, the HIP library);
+        tests pass a CPU double (tests/engine_double.py) to run the multi-rank path over gloo."""
         if on_error not in ('raise', 'skip'):
             raise ValueError('on_error must be "raise" or "skip"')
         self.root, self.job, self.device = root, job, device
@@ -58,17 +65,49 @@ class LocalJob:
         self.settings_path = os.path.join(root, IN_SETTINGS % job)
         self.grid_fn = os.path.join(root, OUT_GRID % job)
         self.out_dir = os.path.join(root, OUT_RASTS % job)
+        self.engine = engine
+        self._host = None
+        self.host_trendline = None
 
     def _path(self, key):
         return os.path.join(self.root, key)
 
+    @staticmethod
+    def _dist():
+        """(torch.distributed or None, world size, rank)."""
+        try:
+            import torch.distributed as dist
+            if dist.is_available() and dist.is_initialized():
+                return dist, dist.get_world_size(), dist.get_rank()
+        except ImportError:
+            pass
+        return None, 1, 0
+
     # 1. setup_mapper
     def setup(self):
+        """Rank 0 extracts the rasters into work_dir and writes the grid (a temporary file moved
+        into place); the other ranks wait for it, then list the same files."""
         rdir = os.path.join(self.root, IN_RASTS % self.job)
         names = sorted(os.listdir(rdir)) if os.path.isdir(rdir) else []
         rasts = analysis_rasters(names)
         if not rasts:
             raise Exception('No analysis rasters specified for job %s' % self.job)
+        dist, _, rank = self._dist()
+        if rank == 0:
+            self._locate(rdir, rasts)
+            os.makedirs(os.path.dirname(self.grid_fn), exist_ok=True)
+            tmp = '%s.tmp%d' % (self.grid_fn, os.getpid())
+            rast2grid(self.rast_fns[0], out_csv=tmp)
+            os.replace(tmp, self.grid_fn)
+        if dist is not None:
+            dist.barrier()
+        if rank != 0:
+            self._locate(rdir, rasts)  # every archive is extracted by now: only listed
+        with open(self.settings_path) as f:
+            self.settings = json.load(f)
+        return self.rast_fns
+
+    def _locate(self, rdir, rasts):
         os.makedirs(self.work_dir, exist_ok=True)
         self.rast_fns, self.mask_fns = [], []
         for n in rasts:
@@ -78,11 +117,6 @@ class LocalJob:
             # parse_mapper: a mask that cannot be fetched is ignored (:59-63)
             self.mask_fns.append(rast_local(mp, self.work_dir) if m != n and os.path.exists(mp)
                                  else None)
-        os.makedirs(os.path.dirname(self.grid_fn), exist_ok=True)
-        rast2grid(self.rast_fns[0], out_csv=self.grid_fn)
-        with open(self.settings_path) as f:
-            self.settings = json.load(f)
-        return self.rast_fns
 
     # 2. parse_mapper
     def parse(self):
@@ -94,10 +128,13 @@ class LocalJob:
     # 3. analysis_reducer, batched over pixel tiles: the mosaic path (runner.py) bench.py runs
     def analyze(self):
         """Tiles of the grid dealt round-robin over the torch.distributed ranks (one when not
-        initialised), analysed by runner.MosaicRunner; every output plane goes to rank 0 (the
-        writer) through the LabelExchange. Returns the host planes on rank 0, None elsewhere."""
+        initialised), analysed by runner.MosaicRunner. The label planes (and status / n_years) go
+        to rank 0, the writer, through the LabelExchange; the per-year trendline planes leave the
+        GPU per tile, while the next tile computes, into host planes [Y, P] (file-backed maps in
+        work_dir, shared by the ranks, when there are several): no GPU ever holds the whole
+        job's trendline. Returns the writer's label planes (device), None on the other ranks."""
         import torch
-        from .distributed import Mosaic
+        from .distributed import Mosaic, TrendlineStream
         from .engine import LABELS, TRENDLINE, get_engine
         from .index_eqn import IndexProgram
         from .runner import MosaicRunner, TileInput
@@ -105,25 +142,26 @@ class LocalJob:
         from .settings import compile_params
         st = self.stack
         P = st['n_pix']
-        dist, world, rank = None, 1, 0
-        if torch.distributed.is_available() and torch.distributed.is_initialized():
-            dist = torch.distributed
-            world, rank = dist.get_world_size(), dist.get_rank()
-        dev = torch.device('cuda', self.device if self.device is not None else
-                           torch.cuda.current_device())
-        fields = LABELS + ('status', 'n_years') + (TRENDLINE if self.trendline else ('winner',))
+        dist, world, rank = self._dist()
+        if self.engine is None:
+            self.engine = get_engine(self.device if self.device is not None else
+                                     torch.cuda.current_device())
+        eng = self.engine
+        dev = torch.device(eng.device)
+        cuda = dev.type == 'cuda'
+        label_fields = LABELS + ('status', 'n_years')
+        tl_fields = TRENDLINE if self.trendline else ('winner',)
         self.scene = build_scene(st['dates'], parse_date(self.settings['target_date']))
         params, self.rules = compile_params(self.settings['line_cost'],
                                             self.settings.get('label_rules', ()),
                                             self.pre_threshold_mode)
-        eng = get_engine(dev)
         numbers = list(st['band_numbers'])
         prog = IndexProgram(self.settings['index_eqn'], band_dtype=st['bands'].dtype,
                             raster_count=max(numbers))
         slots = [numbers.index(b) for b in prog.bands]  # the planes the equation reads
         fn = eng.compile_index(prog)
         m = Mosaic([P], self.tile_pixels, world, rank, 'round_robin')
-        K = self.scene.n_obs
+        K, Y = self.scene.n_obs, self.scene.n_years
         items = []
         for t in m.mine:
             bands = torch.from_numpy(np.ascontiguousarray(
@@ -131,24 +169,68 @@ class LocalJob:
             valid = torch.from_numpy(np.ascontiguousarray(st['valid'][:, t.p0:t.p1])).to(dev)
             vals = torch.empty((K, t.n), dtype=bands.dtype, device=dev)
             items.append(TileInput(t, self.scene, vals, valid, bands))
-        runner = MosaicRunner(eng, m, params, items, fields, fn, dist, exchange_fields=fields)
-        runner.step()
-        torch.cuda.synchronize(dev)
+        host = self.host_trendline = self._trendline_planes(tl_fields, Y, P, dist, world, rank)
+        runner = MosaicRunner(eng, m, params, items, label_fields + tl_fields, fn, dist,
+                              exchange_fields=label_fields)
+
+        def sink(f, row, view, t):  # one completed year row of tile t
+            host[f][row, t.p0:t.p1] = view.numpy().view(host[f].dtype)
+
+        tls = TrendlineStream(m.tile * 8, dev, depth=16, sink=sink) if cuda else None
+
+        def push(k):
+            t = items[k].tile
+            tls.push({f: runner.outs[k][f] for f in tl_fields}, t.n, t)
+
+        # tile k-1's rows are queued behind tile k's kernels, so the copies overlap them
+        runner.step(after_tile=(lambda k: push(k - 1) if k > 0 else None) if cuda else None)
+        if cuda:
+            if items:
+                push(len(items) - 1)
+            torch.cuda.synchronize(dev)
+            tls.drain()
+        else:  # a CPU engine (tests): its planes are host tensors already
+            for o, it in zip(runner.outs, items):
+                for f in tl_fields:
+                    host[f][:, it.tile.p0:it.tile.p1] = o[f][:, :it.tile.n].numpy()
+        for a in host.values():
+            if isinstance(a, np.memmap):
+                a.flush()
+        if dist is not None:
+            dist.barrier()  # every rank's trendline rows are in the shared maps
         self._host = None
         if not runner.exchange.is_writer:
             self.dev_planes = None
             return None
-        # the writer's planes stay in HBM: the output step assembles each raster there
-        self.dev_planes = {f: runner.exchange.raster(f) for f in fields}
-        self.engine = eng
+        # the writer's label planes stay on the device: the output step assembles each raster
+        self.dev_planes = {f: runner.exchange.raster(f) for f in label_fields}
+        del runner
         self._check_errors()
         return self.dev_planes
 
+    def _trendline_planes(self, fields, Y, P, dist, world, rank):
+        """Host [Y, P] planes the trendline rows stream into: in memory for one rank, else
+        file-backed maps in work_dir that rank 0 creates and every rank fills with its tiles."""
+        from .engine import _DTYPE
+        np_dt = {f: np.dtype(str(_DTYPE[f]).replace('torch.', '')) for f in fields}
+        if world == 1:
+            return {f: np.empty((Y, P), np_dt[f]) for f in fields}
+        d = os.path.join(self.work_dir, 'trendline')
+        path = {f: os.path.join(d, f + '.bin') for f in fields}
+        if rank == 0:
+            os.makedirs(d, exist_ok=True)
+            for f in fields:
+                np.memmap(path[f], np_dt[f], 'w+', shape=(Y, P)).flush()
+        dist.barrier()
+        return {f: np.memmap(path[f], np_dt[f], 'r+', shape=(Y, P)) for f in fields}
+
     @property
     def planes(self):
-        """Host copies of the writer's output planes (made on first use)."""
+        """Host copies of the writer's output planes (made on first use): the label planes and
+        the trendline planes."""
         if self._host is None and self.dev_planes is not None:
             self._host = {f: t.cpu().numpy() for f, t in self.dev_planes.items()}
+            self._host.update({f: np.asarray(a) for f, a in self.host_trendline.items()})
         return self._host
 
     def _check_errors(self):
@@ -172,8 +254,7 @@ class LocalJob:
         else:  # skip: the failing pixels emit nothing
             idx = torch.from_numpy(bad).to(self.dev_planes['matched'].device)
             self.dev_planes['matched'][:, idx] = 0
-            if 'winner' in self.dev_planes:
-                self.dev_planes['winner'][:, idx] = -1
+            self.host_trendline['winner'][:, bad] = -1  # no trendline key either
             self._host = None
 
     # 4. output_reducer
@@ -202,7 +283,8 @@ class LocalJob:
         dp['matched'].masked_fill_(empty[None, :], 0)
         self._host = None
         names = [d.strftime('%Y-%m-%d') for d in self.scene.dates]
-        if len(np.unique(dest)) == len(dest) and len(set(names)) == len(names):
+        cuda = torch.device(self.engine.device).type == 'cuda'
+        if cuda and len(np.unique(dest)) == len(dest) and len(set(names)) == len(names):
             ddest = torch.from_numpy(np.ascontiguousarray(dest, np.int64)).to(dp['status'].device)
             out = {}
 
@@ -213,7 +295,8 @@ class LocalJob:
                                              tdt, self.raster_mode).items():
                 write(k, a)
             if self.trendline:
-                trendline_rasters_device(self.engine, dp, self.scene, self.scene.dates,
+                rows_dev = _DeviceRows(self.host_trendline, dp['status'].device)
+                trendline_rasters_device(self.engine, rows_dev, self.scene, self.scene.dates,
                                          (rows, cols), ddest, tdt, self.raster_mode, sink=write)
             return out
         n = rows * cols
@@ -237,6 +320,39 @@ class LocalJob:
         if self.analyze() is None:
             return None
         return self.output()
+
+
+class _DeviceRows:
+    """The host trendline planes as raster.trendline_rasters_device reads them: 'winner' whole on
+    the device (it selects the pixels of every key), every other plane one year row at a time,
+    uploaded into a buffer of its own when the row is asked for (the rows of one date's rasters
+    are assembled together, then the next date's rows overwrite them in stream order)."""
+
+    def __init__(self, host, device):
+        import torch
+        self.host, self.device = host, device
+        self.winner = torch.from_numpy(np.ascontiguousarray(host['winner'])).to(device)
+        self.buf = {}
+
+    def __getitem__(self, field):
+        if field == 'winner':
+            return self.winner
+        return _Rows(self, field)
+
+
+class _Rows:
+    def __init__(self, owner, field):
+        self.owner, self.field = owner, field
+
+    def __getitem__(self, y):
+        import torch
+        o = self.owner
+        row = torch.from_numpy(np.ascontiguousarray(o.host[self.field][y]))
+        b = o.buf.get(self.field)
+        if b is None:
+            b = o.buf[self.field] = torch.empty(row.shape, dtype=row.dtype, device=o.device)
+        b.copy_(row)
+        return b
 
 
 def main(argv=None):

@@ -13,6 +13,7 @@ For every tile this rank owns (distributed.Mosaic), in tile order:
 bench.py, the job runner (job.py) and the GPU tests all run this one code path.
 """
 import contextlib
+import os
 from dataclasses import dataclass
 from typing import Optional
 
@@ -77,7 +78,8 @@ class MosaicRunner:
             raise ValueError('band inputs need a compiled index_eqn (index_fn)')
         # (a CPU engine — the gloo tests' oracle double — has no streams: everything is serial)
         self.cuda = torch.device(engine.device).type == 'cuda'
-        self.load_stream = (torch.cuda.Stream(engine.device)
+        prio = int(os.environ.get('LT_LOAD_PRIORITY', '0'))
+        self.load_stream = (torch.cuda.Stream(engine.device, priority=prio)
                             if self.cuda and has_bands and load_stream else None)
         self.index_events = []  # (start, stop) pairs of the timed steps' load kernels
 
@@ -141,6 +143,11 @@ class MosaicRunner:
                 self.exchange.post(k)
                 if after_tile is not None:
                     after_tile(k)
+        # rounds past this rank's own tiles: the writer still receives the tiles of ranks that
+        # own more (unequal scenes under by_scene, or a writer other than rank 0); a sender has
+        # nothing left to post
+        for k in range(len(self.items), self.m.rounds):
+            self.exchange.post(k)
         self.exchange.wait()
 
     def index_ms(self):

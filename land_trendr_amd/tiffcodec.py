@@ -106,8 +106,9 @@ def undo_predictor(block, predictor, dtype, width, spp):
     if predictor == 3:  # floating point: bytes split into planes (MSB first), then differenced
         rows = block.shape[0]
         item = dtype.itemsize
-        raw = block.view(np.uint8).reshape(rows, width * spp * item)
-        raw = np.cumsum(raw, axis=1, dtype=np.uint8)
+        # libtiff's fpAcc: the byte differencing runs with a stride of one pixel (spp bytes)
+        raw = block.view(np.uint8).reshape(rows, width * item, spp)
+        raw = np.cumsum(raw, axis=1, dtype=np.uint8).reshape(rows, width * spp * item)
         planes = raw.reshape(rows, item, width * spp)
         be = planes.transpose(0, 2, 1)  # [rows, samples, bytes MSB first]
         out = np.ascontiguousarray(be).view(dtype.newbyteorder('>')).reshape(rows, width * spp)

@@ -1,5 +1,5 @@
-// stamp_probe.h — PROFILING BUILD ONLY (profiles/stamps.sh force-includes it into lt_abi.hip
-// with -DLT_ANALYZE_PROBE=StampProbe). Per phase of analyze_fast (lt_fast.h probe.mark), the
+// stamp_probe.h — PROFILING BUILD ONLY (profiles/stamps.sh force-includes it into the profiling
+// dispatch unit with LT_PROBE=StampProbe). Per phase of analyze_fast (lt_fast.h probe.mark), the
 // shader cycles each wave spends there (s_memtime deltas), summed over waves with one atomic per
 // wave and phase, plus the wave count. Results unchanged: the probe only reads the clock.
 #pragma once

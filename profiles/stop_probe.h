@@ -1,5 +1,5 @@
-// stop_probe.h — PROFILING BUILDS ONLY (profiles/phases.sh force-includes it into lt_abi.hip with
-// -DLT_ANALYZE_PROBE=StopProbe<K>): the analyze kernel cut after phase K (lt_fast.h probe), so
+// stop_probe.h — PROFILING BUILDS ONLY (profiles/phases.sh force-includes it into the profiling
+// dispatch unit, LT_PROBE=StopProbe<K>): the analyze kernel cut after phase K (lt_fast.h probe), so
 // PMC counts of builds K = 0..3 and of the product give each phase's instructions by difference.
 #pragma once
 template <int K>

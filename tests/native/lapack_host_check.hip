@@ -31,7 +31,7 @@ extern "C" int ltx_analyze_tile(const lt_scene* sc, const lt_params* prm, const 
   S.n_years = sc->n_years;
   for (int y = 0; y < sc->n_years; y++) {
     S.year[y] = sc->year[y];
-    S.feb29_bad[y] = sc->feb29_bad ? sc->feb29_bad[y] : 0;
+    if (sc->feb29_bad && sc->feb29_bad[y]) S.feb29_mask |= 1ull << y;
   }
   for (int y = 0; y <= sc->n_years; y++) S.slot_begin[y] = sc->n_years ? sc->slot_begin[y] : 0;
   for (int k = 0; k < sc->n_obs; k++) {

@@ -1,7 +1,9 @@
 """Multi-process (gloo, CPU) checks of the mosaic path bench.py and the job runner use:
 distributed.Mosaic tiling, runner.MosaicRunner's per-rank pipeline and distributed.LabelExchange's
-point-to-point sends to the writer. The per-tile compute is the CPU oracle (test infrastructure)
-behind a stand-in for the HIP engine (OracleEngine); on a GPU job it is liblt_hip.so."""
+point-to-point sends to the writer, and the multi-rank local job (job.LocalJob: rank-0 setup, label
+exchange, trendline rows through the shared host maps). The per-tile compute is the CPU oracle (test
+infrastructure) behind a stand-in for the HIP engine (tests/engine_double.py); on a GPU job it is
+liblt_hip.so."""
 import os
 import socket
 
@@ -12,31 +14,11 @@ import torch.multiprocessing as mp
 
 from land_trendr_amd import distributed as ltd
 
+from engine_double import OracleEngine
+
 RULES = [{'name': 'gd', 'val': 1, 'change_type': 'GD'},
          {'name': 'fd', 'val': 2, 'change_type': 'FD', 'duration': ['<', 5]}]
 FIELDS = ('status', 'matched', 'class_val', 'onset_year', 'duration', 'magnitude')
-
-
-class OracleEngine:
-    """Engine stand-in on the CPU: index_tile evaluates the IndexProgram with numpy
-    (oracle/index_oracle.py), analyze_tiles runs oracle/lt_oracle.c into the given outputs."""
-    device = torch.device('cpu')
-
-    def index_tile(self, fn, bands, out=None, stream=None):
-        from oracle import index_oracle
-        b = bands.numpy()
-        v = index_oracle.evaluate(fn.program, np.moveaxis(b, 1, 0))
-        out.copy_(torch.from_numpy(np.ascontiguousarray(v)))
-        return out
-
-    def analyze_tiles(self, scene, params, tiles, fields, outs=None, ready=None):
-        from oracle import oracle
-        for (vals, valid), o in zip(tiles, outs):
-            want = oracle.analyze_tile(scene, params, vals.numpy().astype(np.float64),
-                                       None if valid is None else valid.numpy())
-            for f in fields:
-                o[f].copy_(torch.from_numpy(want[f][..., :o[f].shape[-1]]))
-        return outs
 
 
 def _free_port():
@@ -47,7 +29,7 @@ def _free_port():
     return port
 
 
-def _run(world, rank, scene_px, tile, assign, seed0, dist=None):
+def _run(world, rank, scene_px, tile, assign, seed0, dist=None, dst=0):
     from land_trendr_amd.engine import IndexFn
     from land_trendr_amd.index_eqn import IndexProgram
     from land_trendr_amd.runner import MosaicRunner
@@ -57,18 +39,18 @@ def _run(world, rank, scene_px, tile, assign, seed0, dist=None):
     items = mosaic_inputs(m, 20, 1, 2, 0.1, seed0, 'cpu')
     params, _ = compile_params(10, RULES)
     fn = IndexFn(None, IndexProgram('B1 - B2', band_dtype='int16'))
-    r = MosaicRunner(OracleEngine(), m, params, items, FIELDS, fn, dist)
+    r = MosaicRunner(OracleEngine(), m, params, items, FIELDS, fn, dist, dst=dst)
     r.step()
     return r
 
 
-def _worker(rank, world, port, scene_px, tile, assign, result_path):
+def _worker(rank, world, port, scene_px, tile, assign, result_path, dst=0):
     import torch.distributed as dist
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(port)
     dist.init_process_group('gloo', rank=rank, world_size=world)
-    r = _run(world, rank, scene_px, tile, assign, 7, dist)
-    if rank == 0:
+    r = _run(world, rank, scene_px, tile, assign, 7, dist, dst)
+    if rank == dst:
         np.savez(result_path, **{f: r.exchange.raster(f).numpy()
                                  for f in ltd.LABEL_GATHER_FIELDS})
     dist.barrier()
@@ -122,16 +104,85 @@ def test_single_process_runner_matches_oracle():
         assert _same(want[f][:2], got), f
 
 
-@pytest.mark.parametrize('world,px,tile,assign', [
-    (2, [700, 300], 256, 'round_robin'),   # the c4 shape: one mosaic, tiles round-robin
-    (2, [600, 600], 256, 'by_scene'),      # the c2 shape: one scene per rank
-    (3, [300], 256, 'round_robin'),        # more ranks than tiles: rank 2 owns nothing
+@pytest.mark.parametrize('world,px,tile,assign,dst', [
+    (2, [700, 300], 256, 'round_robin', 0),  # the c4 shape: one mosaic, tiles round-robin
+    (2, [600, 600], 256, 'by_scene', 0),     # the c2 shape: one scene per rank
+    (3, [300], 256, 'round_robin', 0),       # more ranks than tiles: rank 2 owns nothing
+    # the writer owns fewer tiles than a peer: it must still post the peer's later rounds
+    (2, [300, 900], 256, 'by_scene', 0),     # unequal scenes (writer 2 tiles, peer 4)
+    (2, [700, 300], 256, 'round_robin', 1),  # writer rank 1 (2 tiles) under round-robin (3)
+    (3, [300, 200, 900], 256, 'by_scene', 2),  # writer 4 tiles, peers 2 and 1
 ])
-def test_multi_rank_exchange_matches_single_process(tmp_path, world, px, tile, assign):
+@pytest.mark.timeout(180)  # an unmatched send hangs: fail instead
+def test_multi_rank_exchange_matches_single_process(tmp_path, world, px, tile, assign, dst):
     path = str(tmp_path / 'r.npz')
-    mp.spawn(_worker, args=(world, _free_port(), px, tile, assign, path), nprocs=world,
+    mp.spawn(_worker, args=(world, _free_port(), px, tile, assign, path, dst), nprocs=world,
              join=True)
     got = np.load(path)
     want = _want(px, 7)
     for f in ltd.LABEL_GATHER_FIELDS:
         assert _same(want[f][:2], got[f]), f
+
+
+def _job_worker(rank, world, port, root, result_path):
+    import torch.distributed as dist
+    from land_trendr_amd.geotiff import GeoTiff
+    from land_trendr_amd.job import LocalJob
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    j = LocalJob(root, 'synth', tile_pixels=20, on_error='skip', engine=OracleEngine())
+    files = j.run()
+    if rank == 0:
+        arrs = {'raster:' + k: GeoTiff(v[0]).read() for k, v in files.items()}
+        arrs.update({'plane:' + k: a for k, a in j.planes.items()})
+        np.savez(result_path, **arrs)
+    else:
+        assert files is None
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_multi_rank_job_matches_single_rank_and_oracle(tmp_path):
+    """job.LocalJob over 2 gloo ranks (tar.gz inputs extracted by rank 0 alone, tiles
+    round-robin, labels exchanged to rank 0, trendline rows through the shared host maps): every
+    output raster equals the single-rank job's, and the planes equal the oracle's."""
+    from jobfixture import SETTINGS, make_job
+    from land_trendr_amd import _abi
+    from land_trendr_amd.geotiff import GeoTiff
+    from land_trendr_amd.job import LocalJob
+    from land_trendr_amd.scene import build_scene, parse_date
+    from land_trendr_amd.settings import compile_params
+    from oracle import oracle
+    multi, single = str(tmp_path / 'multi'), str(tmp_path / 'single')
+    make_job(multi)
+    make_job(single)
+    path = str(tmp_path / 'job.npz')
+    mp.spawn(_job_worker, args=(2, _free_port(), multi, path), nprocs=2, join=True)
+    got = dict(np.load(path))
+    j = LocalJob(single, 'synth', tile_pixels=1 << 20, on_error='skip', engine=OracleEngine())
+    files = j.run()
+    assert sorted('raster:' + k for k in files) == sorted(k for k in got if k.startswith('raster:'))
+    assert any(k.startswith('trendline/') for k in files)
+    for k, v in files.items():
+        assert np.array_equal(GeoTiff(v[0]).read(), got['raster:' + k]), k
+    st = j.stack
+    idx = (st['bands'][:, 0, :].astype(np.int32) - st['bands'][:, 1, :]).astype(np.int16)
+    meta = build_scene(st['dates'], parse_date(SETTINGS['target_date']))
+    params, _ = compile_params(SETTINGS['line_cost'], SETTINGS['label_rules'])
+    exp = oracle.analyze_tile(meta, params, idx.astype(np.float64), st['valid'])
+    bad = np.flatnonzero(exp['status'] & ~_abi.LT_ST_EMPTY)  # on_error='skip'
+    exp['matched'][:, bad] = 0
+    exp['winner'][:, bad] = -1
+    for k in [k for k in got if k.startswith('plane:')]:
+        a, e = got[k], exp[k[6:]]
+        e = e[:a.shape[0]] if a.ndim == 2 else e
+        if k[6:] in ('onset_year', 'duration', 'class_val', 'magnitude', 'initial_val'):
+            m = exp['matched'][:a.shape[0]].astype(bool)
+            a, e = np.where(m, a, 0), np.where(m, e, 0)
+        assert _same(a, e) or (a.dtype.kind == 'f' and _same_nan(a, e)), k
+
+
+def _same_nan(a, b):
+    return ((a.view(np.int64) == b.view(np.int64)) | (np.isnan(a) & np.isnan(b))).all()

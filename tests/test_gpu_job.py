@@ -15,7 +15,7 @@ from land_trendr_amd.settings import compile_params
 from oracle import oracle
 
 from golden_io import _bits_equal
-from jobfixture import SETTINGS, make_job
+from jobfixture import SETTINGS, check_job_outputs, make_job
 
 pytestmark = pytest.mark.gpu
 
@@ -64,6 +64,20 @@ def test_local_job_end_to_end(tmp_path, tile):
             got = GeoTiff(files[name][0]).read()[0]
             assert np.array_equal(got, raster.gdal_to_byte(holder)), name
     assert any(k.startswith('trendline/') for k in files)
+
+
+@pytest.mark.parametrize('dtype', [np.int16, np.uint16])
+def test_local_job_output_rasters_match_literal_data2raster(tmp_path, dtype):
+    """Every output raster the GPU assembles (lt_raster_assemble), trendline/<date>-<attr> keys
+    included, against a literal data2raster over the reducer's per-point emissions
+    (jobfixture.literal_output_rasters; mr_land_trendr_job.py:108-152, utils.py:414-440), for an
+    int16 and a uint16 template; tiles of 40 px so several tiles stream their trendline rows."""
+    root = str(tmp_path)
+    make_job(root, dtype=dtype)
+    j = LocalJob(root, 'synth', device=0, tile_pixels=40, on_error='skip')
+    files = j.run()
+    assert GeoTiff(j.rast_fns[0]).dtype == np.dtype(dtype)
+    check_job_outputs(j, files)
 
 
 def test_local_job_raises_like_the_reference(tmp_path):

@@ -150,6 +150,27 @@ def test_bad_equations_raise_like_indexprogram(eqn):
         c_compile(dict(BASE, index_eqn=eqn))
 
 
+@pytest.mark.parametrize('depth', [63, 200, 201, 5000, 100000])
+@pytest.mark.parametrize('kind', ['paren', 'sign', 'sign_const'])
+def test_deep_nesting_is_rejected_not_a_crash(kind, depth):
+    """Nested parentheses / sign chains: the C ABI accepts what the Python host accepts and
+    raises ValueError for the rest (the host's parser stops at 200 parentheses; long sign chains
+    exceed its 64 operations, reference no band, or exhaust the interpreter: RecursionError /
+    MemoryError there), instead of exhausting the native stack."""
+    eqn = {'paren': '(' * depth + 'B1' + ')' * depth, 'sign': '-' * depth + 'B1',
+           'sign_const': '-' * depth + '1 + B1'}[kind]
+    try:
+        IndexProgram(eqn, band_dtype=np.int16).to_c()
+        host_ok = True
+    except (Exception, RecursionError, MemoryError):
+        host_ok = False
+    if host_ok:
+        check_same(dict(BASE, index_eqn=eqn))
+    else:
+        with pytest.raises(ValueError):
+            c_compile(dict(BASE, index_eqn=eqn))
+
+
 def test_settings_keys_and_json():
     with pytest.raises(KeyError):
         c_compile({'target_date': '2014-07-01'})

@@ -111,3 +111,32 @@ def test_lzw_scene_sized_raster_is_fast_enough(tmp_path):
     t2 = time.perf_counter()
     assert np.array_equal(got, a)
     assert t1 - t0 < 30 and t2 - t1 < 30, (t1 - t0, t2 - t1)
+
+
+def _fp_predict(row_bytes, item, spp):
+    """libtiff's fpDiff (PREDICTOR_FLOATINGPOINT encode) of one row of little-endian samples:
+    bytes regrouped into planes, most significant first, then differenced with a stride of one
+    pixel (spp bytes)."""
+    b = np.frombuffer(row_bytes, np.uint8)
+    wc = len(b) // item
+    planes = b.reshape(wc, item)[:, ::-1].T.reshape(-1)  # MSB plane first
+    d = planes.astype(np.int16)
+    d[spp:] = d[spp:] - planes[:-spp].astype(np.int16)
+    return (d & 0xff).astype(np.uint8)
+
+
+@pytest.mark.parametrize('spp', [1, 3])
+@pytest.mark.parametrize('dtype', [np.float32, np.float64])
+def test_floating_point_predictor_undo_with_chunky_bands(spp, dtype):
+    """Predictor 3 on a chunky raster of spp samples per pixel (PlanarConfiguration 1): libtiff
+    accumulates the byte planes with a stride of spp, not 1."""
+    rng = np.random.default_rng(spp)
+    rows, width = 5, 17
+    a = rng.normal(0, 1000, (rows, width * spp)).astype(dtype)
+    item = np.dtype(dtype).itemsize
+    enc = np.stack([_fp_predict(a[r].astype('<' + np.dtype(dtype).str[1:]).tobytes(), item, spp)
+                    for r in range(rows)])
+    block = np.frombuffer(enc.tobytes(), '<' + np.dtype(dtype).str[1:]).reshape(rows, width * spp)
+    got = tiffcodec.undo_predictor(block.copy(), 3, np.dtype('<' + np.dtype(dtype).str[1:]),
+                                   width, spp)
+    assert np.array_equal(got.astype(dtype), a)
