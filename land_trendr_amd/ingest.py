@@ -134,24 +134,42 @@ def serialize_rast(rast_fn, extra_data={}):
             yield point_wkt(x, y), pt_data
 
 
-def grid_wkts(ds):
-    """The WKT column rast2grid writes, vectorised (same operations, same order)."""
+def _grid_text(ds):
+    """The distinct coordinate texts of rast2grid's grid: one per raster column (x) and row (y),
+    the same operations serialize_rast does (utils.py:315-321)."""
     ds = _open(ds)
     top_left_x, pix_width, _, top_left_y, _, pix_height = ds.geotransform()
     xs = top_left_x + (np.arange(ds.width, dtype=np.float64) + 0.5) * pix_width
     ys = top_left_y + (np.arange(ds.height, dtype=np.float64) + 0.5) * pix_height
-    xt = [py2_float_str(v) for v in xs]
-    yt = [py2_float_str(v) for v in ys]
+    return [py2_float_str(v) for v in xs], [py2_float_str(v) for v in ys]
+
+
+def grid_wkts(ds):
+    """The WKT column rast2grid writes, vectorised (same operations, same order)."""
+    xt, yt = _grid_text(ds)
     return ['POINT(%s %s)' % (a, b) for a in xt for b in yt]
+
+
+def grid_coords(ds):
+    """grid_points of the grid rast2grid writes for raster `ds`, without the text round trip per
+    point: each distinct coordinate text (one per column and per row) is parsed once, as OGR /
+    float() parse it, and laid out in the grid's order (columns outer, rows inner). Equal to
+    grid_points(rast2grid(ds)) (tests/test_ingest.py)."""
+    xt, yt = _grid_text(ds)
+    xv = np.array([float(t) for t in xt], np.float64)
+    yv = np.array([float(t) for t in yt], np.float64)
+    return np.repeat(xv, len(yv)), np.tile(yv, len(xv))
 
 
 def rast2grid(rast_fn, out_csv='/tmp/grid.csv'):
     """utils.rast2grid (utils.py:361-370): CSV with a 'pix_ctr_wkt' column, one pixel centre per
     line (pandas to_csv, index=False: no quoting is needed for 'POINT(x y)')."""
+    xt, yt = _grid_text(rast_fn)
     with open(out_csv, 'w') as f:
         f.write('pix_ctr_wkt\n')
-        for w in grid_wkts(rast_fn):
-            f.write(w + '\n')
+        for a in xt:  # one column of points (rows inner) per join
+            pre = 'POINT(%s ' % a
+            f.write(pre + (')\n' + pre).join(yt) + ')\n')
     return out_csv
 
 
@@ -222,43 +240,99 @@ def analysis_rasters(paths):
     return sorted(p for p in paths if RAST_TRIGGER in os.path.basename(p))
 
 
-def ingest_stack(rast_fns, grid, mask_fns=None, bands=None):
+def host_threads():
+    """CPU threads this process should use: its affinity set, capped by the cgroup CPU quota when
+    one is set (a GPU box shows the whole machine's CPUs but grants each job a share)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    try:
+        q, per = open('/sys/fs/cgroup/cpu.max').read().split()[:2]
+        if q != 'max':
+            n = max(1, min(n, -(-int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+class _Offsets:
+    """grid_offsets per distinct (geotransform, shape), computed once (a stack's rasters nearly
+    all share one), with whether the grid is the raster's own pixels in order (then sampling is
+    a plain copy)."""
+
+    def __init__(self, lng, lat):
+        import threading
+        self.lng, self.lat = lng, lat
+        self.cache = {}
+        self.lock = threading.Lock()
+
+    def __call__(self, ds):
+        key = (ds.geotransform(), ds.height, ds.width)
+        with self.lock:
+            hit = self.cache.get(key)
+            if hit is None:
+                idx, ok = grid_offsets(key[0], (ds.height, ds.width), self.lng, self.lat)
+                ident = bool(ok.all()) and len(idx) == ds.height * ds.width and bool(
+                    (idx == np.arange(len(idx))).all())
+                hit = self.cache[key] = (idx, ok, ident)
+        return hit
+
+
+def ingest_stack(rast_fns, grid, mask_fns=None, bands=None, threads=None):
     """parse_mapper over every analysis raster, as planes for analysis_reducer_batch.
 
     rast_fns: the (decompressed) analysis rasters, in the mapper order that becomes each pixel's
-    observation order; grid: CSV path or WKT list (P points); mask_fns: per raster the mask path
-    or None (default: mask_name(fn) when that file exists); bands: the band numbers to gather
-    (default: all bands of each raster).
+    observation order; grid: CSV path, WKT list or (lng, lat) arrays (P points); mask_fns: per
+    raster the mask path or None (default: mask_name(fn) when that file exists); bands: the band
+    numbers to gather (default: all bands of each raster); threads: decode / gather workers
+    (default host_threads(): the codecs and the gathers release the GIL).
     Returns dict(dates=['YYYY-MM-DD'] * K, bands=[K, nb, P] in the rasters' sample type,
     band_numbers=[nb], valid=[K, P] uint8)."""
-    lng, lat = grid_points(grid)
+    from concurrent.futures import ThreadPoolExecutor
+    lng, lat = grid if isinstance(grid, tuple) else grid_points(grid)
     P = len(lng)
     K = len(rast_fns)
     if mask_fns is None:
         mask_fns = [mask_name(f) if os.path.exists(mask_name(f)) and mask_name(f) != f else None
                     for f in rast_fns]
-    out_bands, valid, dates, dtype, numbers = None, np.zeros((K, P), np.uint8), [], None, None
-    for k, fn in enumerate(rast_fns):
-        ds = _open(fn)
-        a = ds.read()
-        if numbers is None:
-            numbers = list(bands) if bands is not None else list(range(1, ds.bands + 1))
-            dtype = a.dtype
-            out_bands = np.zeros((K, len(numbers), P), dtype)
-        if a.dtype != dtype:
-            raise ValueError('%s: sample type %s differs from the stack\'s %s' % (fn, a.dtype, dtype))
+    if K == 0:
+        return dict(dates=[], bands=np.zeros((0, 0, P)), band_numbers=list(bands or []),
+                    valid=np.zeros((0, P), np.uint8), n_pix=P)
+    first = _open(rast_fns[0])
+    numbers = list(bands) if bands is not None else list(range(1, first.bands + 1))
+    dtype = first.dtype.newbyteorder('=')
+    out_bands = np.empty((K, len(numbers), P), dtype)
+    valid = np.empty((K, P), np.uint8)
+    offsets = _Offsets(lng, lat)
+    sel = [b - 1 for b in numbers]
+
+    def one(k):
+        fn = rast_fns[k]
+        ds = first if k == 0 else _open(fn)
+        if ds.dtype.newbyteorder('=') != dtype:
+            raise ValueError('%s: sample type %s differs from the stack\'s %s' % (fn, ds.dtype, dtype))
         if max(numbers) > ds.bands:
             raise Exception('Band %s requested but raster only has %s bands' % (max(numbers),
                                                                                  ds.bands))
-        idx, ok = grid_offsets(ds.geotransform(), (ds.height, ds.width), lng, lat)
-        planes = a.reshape(ds.bands, -1)
-        out_bands[k] = planes[[b - 1 for b in numbers]][:, idx] * ok
-        v = ok.copy()
+        planes = ds.read().reshape(ds.bands, -1)
+        idx, ok, ident = offsets(ds)
+        if ident:  # the grid is this raster's pixels in order: a copy
+            out_bands[k] = planes[sel]
+        else:
+            np.take(planes[sel], idx, axis=1, out=out_bands[k])
+            out_bands[k][:, ~ok] = 0
+        v = ok.astype(np.uint8)
         if mask_fns[k]:
             mds = _open(mask_fns[k])
-            midx, mok = grid_offsets(mds.geotransform(), (mds.height, mds.width), lng, lat)
-            mval = mds.read()[0].reshape(-1)[midx]
+            midx, mok, mident = offsets(mds)
+            m = mds.read()[0].reshape(-1)
+            mval = m if mident else m[midx]
             v &= ~(mok & (mval == 0))
         valid[k] = v
-        dates.append(filename2date(fn))
+        return filename2date(fn)
+
+    n = max(1, min(K, threads or host_threads()))
+    with ThreadPoolExecutor(n) as pool:
+        dates = list(pool.map(one, range(K)))
     return dict(dates=dates, bands=out_bands, band_numbers=numbers, valid=valid, n_pix=P)

@@ -38,7 +38,7 @@ import sys
 import numpy as np
 
 from . import _abi
-from .ingest import (analysis_rasters, grid_points, grid_offsets, ingest_stack, mask_name,
+from .ingest import (analysis_rasters, grid_coords, grid_offsets, ingest_stack, mask_name,
                      rast2grid, rast_local, read_grid)
 
 IN_SETTINGS = '%s/input/settings.json'
@@ -103,6 +103,8 @@ class LocalJob:
             dist.barrier()
         if rank != 0:
             self._locate(rdir, rasts)  # every archive is extracted by now: only listed
+        # the grid's point coordinates, as parsing the CSV just written gives them
+        self.grid_xy = grid_coords(self.rast_fns[0])
         with open(self.settings_path) as f:
             self.settings = json.load(f)
         return self.rast_fns
@@ -122,7 +124,7 @@ class LocalJob:
     def parse(self):
         from .index_eqn import parse_eqn_bands
         eqn_bands = sorted(parse_eqn_bands(self.settings['index_eqn']))
-        self.stack = ingest_stack(self.rast_fns, self.grid_fn, self.mask_fns, bands=eqn_bands)
+        self.stack = ingest_stack(self.rast_fns, self.grid_xy, self.mask_fns, bands=eqn_bands)
         return self.stack
 
     # 3. analysis_reducer, batched over pixel tiles: the mosaic path (runner.py) bench.py runs
@@ -270,7 +272,7 @@ class LocalJob:
                              trendline_rasters, trendline_rasters_device)
         tmpl = GeoTiff(self.rast_fns[0])
         rows, cols = tmpl.height, tmpl.width
-        lng, lat = grid_points(self.grid_fn)
+        lng, lat = self.grid_xy
         dest, ok = grid_offsets(tmpl.geotransform(), (rows, cols), lng, lat)
         if not ok.all():
             # data2raster assigns holder[y_off, x_off]: an off-template point raises there

@@ -136,6 +136,26 @@ def test_ingest_stack_matches_per_point_parse(tmp_path):
     assert not st['valid'][3].all()
 
 
+def test_grid_coords_equal_parsing_the_written_grid(tmp_path):
+    """grid_coords (each distinct coordinate text parsed once) equals grid_points of the CSV
+    rast2grid writes, bit for bit, on the reference's fixture and on a job raster."""
+    out = str(tmp_path / 'grid.csv')
+    ingest.rast2grid(TIF, out)
+    for a, b in zip(ingest.grid_coords(TIF), ingest.grid_points(out)):
+        assert a.dtype == b.dtype and np.array_equal(a.view(np.int64), b.view(np.int64))
+    root = str(tmp_path / 'job')
+    make_job(root)
+    j = LocalJob(root, 'synth')
+    j.setup()
+    for a, b in zip(j.grid_xy, ingest.grid_points(j.grid_fn)):
+        assert np.array_equal(a.view(np.int64), b.view(np.int64))
+    # the threaded ingest from coordinates equals a serial one from the CSV
+    st = ingest.ingest_stack(j.rast_fns, j.grid_xy, j.mask_fns, bands=[1, 2])
+    st1 = ingest.ingest_stack(j.rast_fns, j.grid_fn, j.mask_fns, bands=[1, 2], threads=1)
+    assert st['dates'] == st1['dates']
+    assert np.array_equal(st['bands'], st1['bands']) and np.array_equal(st['valid'], st1['valid'])
+
+
 def test_job_setup_errors(tmp_path):
     os.makedirs(tmp_path / 'j' / 'input' / 'rasters')
     with pytest.raises(Exception, match='No analysis rasters'):
