@@ -117,8 +117,8 @@ def test_stage_in_and_trendline_stream_match_resident_path():
             t.fill_(0)
     got = {}
 
-    def sink(f, row, host):
-        got.setdefault(f, []).append((row, host.clone()))
+    def sink(f, row, host, key):
+        got.setdefault(f, []).append((row, host.clone(), key))
 
     stage = bench._PinnedBands(items, eng.device)
     d2h = TrendlineStream(m.tile * 8, eng.device, depth=4, sink=sink)
@@ -127,11 +127,12 @@ def test_stage_in_and_trendline_stream_match_resident_path():
     def after(k):
         if k > 0:
             d2h.push({f: runner.outs[k - 1][f] for f in bench.TRENDLINE_FIELDS},
-                     items[k - 1].tile.n)
+                     items[k - 1].tile.n, key=k - 1)
             pushed.append(k - 1)
 
     runner.step(after_tile=after, stage_in=stage)
-    d2h.push({f: runner.outs[-1][f] for f in bench.TRENDLINE_FIELDS}, items[-1].tile.n)
+    d2h.push({f: runner.outs[-1][f] for f in bench.TRENDLINE_FIELDS}, items[-1].tile.n,
+             key=len(items) - 1)
     pushed.append(len(items) - 1)
     torch.cuda.synchronize()
     d2h.drain()
@@ -147,7 +148,7 @@ def test_stage_in_and_trendline_stream_match_resident_path():
         for j, k in enumerate(pushed):
             n = items[k].tile.n
             for y in range(Y):
-                row, host = rows[j * Y + y]
-                assert row == y
+                row, host, key = rows[j * Y + y]
+                assert row == y and key == k
                 want = ref[k][f][y, :n].cpu().contiguous().view(torch.uint8)
                 assert torch.equal(host, want), (f, k, y)
