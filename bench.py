@@ -75,10 +75,11 @@ def f_ref(n):
     return 20 * s3 + n * (n + 1) + 24 * n
 
 
-def bytes_per_pixel(cfg, n_obs, n_years):
-    """Algorithmic HBM bytes per pixel of the analyze kernel: the int16 index raster (+ mask),
-    the label planes, the per-year planes when the config asks for them, status."""
-    inp = n_obs * 2 + (n_obs if cfg['mask'] > 0 else 0)
+def bytes_per_pixel(cfg, n_obs, n_years, fused=True):
+    """Algorithmic HBM bytes per pixel of the analyze kernel: the inputs (the two int16 band
+    planes with the fused load stage, else the int16 index raster; + mask), the label planes, the
+    per-year planes when the config asks for them, status."""
+    inp = n_obs * (4 if fused else 2) + (n_obs if cfg['mask'] > 0 else 0)
     lab = len(cfg['rules']) * (1 + 4 + 4 + 4 + 8)                 # matched/class/onset/dur/mag
     tl = n_years * (6 * 8 + 2 + 2) if cfg['trendline'] else 0     # 6 f64 + spike/vertex + winner
     return inp + lab + tl + 4
@@ -172,6 +173,8 @@ def parity_sample(runner, params, n_sample, threads, seed=12345):
     bad, per_field, checked = 0, {}, 0
     for k in np.unique(tile_of):
         it = items[k]
+        if runner.fused:  # the fused steps read the band planes: the load kernel's raster of them
+            runner.materialise_index(k)
         cols = torch.from_numpy(flat[tile_of == k] - starts[k]).to(it.values.device)
         vals = it.values[:, cols].double().cpu().numpy()
         valid = None if it.valid is None else it.valid[:, cols].cpu().numpy()
@@ -194,14 +197,27 @@ def parity_sample(runner, params, n_sample, threads, seed=12345):
     return checked, bad, per_field
 
 
+def _pinned_like(t):
+    """A pinned, compact host copy of the [K, NB, n] bands t in t's layout: planar, or
+    pixel-interleaved (a [K, n, NB] buffer viewed as [K, NB, n])."""
+    K, NB, n = t.shape
+    if t.stride(1) == 1 and NB > 1:
+        h = torch.empty((K, n, NB), dtype=t.dtype, pin_memory=True).permute(0, 2, 1)
+    else:
+        h = torch.empty((K, NB, n), dtype=t.dtype, pin_memory=True)
+    h.copy_(t)
+    return h
+
+
 class _PinnedBands:
     """stage_in for MosaicRunner.step: tile k's int16 bands H2D from pinned host memory into
     device slab k % 2 on a copy stream, once the load kernel of tile k - 2 has read that slab."""
 
     def __init__(self, items, dev):
-        self.host = [it.bands.cpu().pin_memory() for it in items]
+        # host copies and device slabs in the bands' own layout (planar or pixel-interleaved)
+        self.host = [_pinned_like(it.bands) for it in items]
         big = max(self.host, key=lambda b: b.numel())
-        self.slab = [torch.empty(big.shape, dtype=torch.int16, device=dev) for _ in range(2)]
+        self.slab = [torch.empty_like(big, device=dev) for _ in range(2)]
         self.free = [None, None]
         self.stream = torch.cuda.Stream(dev)
         self.bytes = 0
@@ -313,8 +329,11 @@ def main():
     else:  # one scene per rank (weak scaling)
         tile = args.tile or (1 << 24)
         mosaic = Mosaic([P] * world, tile, world, rank, 'by_scene')
+    fused = os.environ.get('LT_FUSED_INDEX', '1') != '0'
     items = mosaic_inputs(mosaic, cfg['years'], cfg['k'][0], cfg['k'][1], cfg['mask'],
-                          cfg['seed'], dev, TARGET)
+                          cfg['seed'], dev, TARGET,
+                          band_layout=os.environ.get('LT_BAND_LAYOUT',
+                                                     'pixel' if fused else 'planar'))
     params, rules = compile_params(cfg['line_cost'], cfg['rules'], cfg['mode'])
     eng = get_engine(local)
     index_fn = eng.compile_index(IndexProgram('B1 - B2', band_dtype='int16'))
@@ -368,7 +387,8 @@ def main():
                    'fields': sorted(runner.fields), 'mismatches_rank0': per_field,
                    'seconds_rank0': round(time.perf_counter() - t_ps, 2),
                    'checker': 'oracle/lt_oracle.c on a seeded sample of each rank\'s pixels, '
-                              'from the index rasters the timed steps read'}
+                              'from the index rasters of the bands the timed steps read '
+                              '(lt_index_apply)'}
     # the load kernel alone (its HBM roofline): one tile, serially, after the timed region
     it0 = items[0]
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
@@ -426,7 +446,7 @@ def main():
             f64_px = 64 * (a['SQ_INSTS_VALU_ADD_F64'] + a['SQ_INSTS_VALU_MUL_F64'] +
                            2 * a['SQ_INSTS_VALU_FMA_F64']) / pmc['_pixels_per_launch']
     traffic_px = per_px(pmc, 'analyze', 'hbm_bytes')
-    bpp = bytes_per_pixel(cfg, meta.n_obs, meta.n_years)
+    bpp = bytes_per_pixel(cfg, meta.n_obs, meta.n_years, runner.fused)
     hbm_gbs = bpp * px_per_launch / (kern_ms * 1e-3) / 1e9
     ref_equiv = f_ref(cfg['years']) * px_per_launch / (kern_ms * 1e-3) / 1e12
 
@@ -445,7 +465,8 @@ def main():
                    'obs': meta.n_obs, 'rules': len(rules), 'line_cost': cfg['line_cost'],
                    'tile_pixels': tile, 'tiles': len(mosaic.tiles), 'tiles_rank0': len(items),
                    'gather': bool(gather),
-                   'input': 'int16 bands B1, B2 + index_eqn "B1 - B2"',
+                   'input': 'int16 bands B1, B2 + index_eqn "B1 - B2"' +
+                            (' (fused into the analyze kernel)' if runner.fused else ''),
                    'parallelism': ('one mosaic, tiles round-robin over %d GPU(s), labels sent '
                                    'to rank 0' % world) if mosaic_cfg else
                                   ('one scene per GPU (%d), labels sent to rank 0' % world)},
@@ -479,7 +500,11 @@ def main():
         'status_numeric_pixels': n_numeric,
         'parity_sample': psample,
         'load_stage': {
-            'kernel': 'lt_index_kernel4 (hiprtc, index_eqn "B1 - B2", int16 bands -> int16)',
+            'fused': runner.fused,
+            'kernel': ('analyze_fast_kernel (index_eqn "B1 - B2" as lt_index_lin, evaluated on '
+                       'each winner\'s band values; lt_index_kernel4 below only for comparison)'
+                       if runner.fused else
+                       'lt_index_kernel4 (hiprtc, index_eqn "B1 - B2", int16 bands -> int16)'),
             'ms_per_launch_overlapped': r(index_ms, 3),
             'alone': {'ms': round(index_alone_ms, 4), 'pixels': it0.tile.n,
                       'bytes': index_bytes,

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define LT_ABI_VERSION 3
+#define LT_ABI_VERSION 4
 #define LT_MAX_YEARS 64   /* distinct calendar years per scene (T <= 40 in every config) */
 #define LT_MAX_OBS 1024   /* observations per scene (K*T) */
 #define LT_MAX_RULES 16
@@ -95,6 +95,22 @@ typedef struct {
 /* Element types of raster planes (the GDAL band types a LandTrendr stack meets). */
 enum { LT_T_F64 = 0, LT_T_I16 = 1, LT_T_U16 = 2, LT_T_I32 = 3, LT_T_F32 = 4, LT_T_U8 = 5,
        LT_T_U32 = 6, LT_T_I8 = 7, LT_T_I64 = 8 };
+/* An index_eqn program that is an integer linear form (lt_index_linearize): every arithmetic
+ * node has the one integer type wrap_type, multiplications have a constant side, no division.
+ * Its value for bands b[0..n_bands) is store_out(wrap(c0 + sum coef[s] * b[s])), the sum taken
+ * modulo 2^64 (exact modulo 2^bits(wrap_type), as numpy's wrapping node by node), store_out the
+ * load stage's store into out_type (lt_index.h). The analyze kernel evaluates it on the winning
+ * observations' band values, so the index raster is never written (lt_tile_in.obs_bands). */
+#define LT_LIN_MAX_BANDS 4
+typedef struct {
+  int32_t n_bands;            /* band planes the form reads (<= LT_LIN_MAX_BANDS)            */
+  int32_t band_type;          /* LT_T_* of the band planes (I16 / U16 / U8 / I32)            */
+  int32_t wrap_type;          /* LT_T_* of every arithmetic node                             */
+  int32_t out_type;           /* LT_T_* of the index raster the form stands for              */
+  int64_t c0;                 /* constant term, modulo 2^64                                  */
+  int64_t coef[LT_LIN_MAX_BANDS]; /* coefficient of band plane s, modulo 2^64                */
+} lt_index_lin;
+
 typedef struct {
   int64_t n_pix;              /* P                                                          */
   int64_t stride;             /* elements between obs planes (>= n_pix)                     */
@@ -104,6 +120,17 @@ typedef struct {
                               /* what lt_index_apply wrote); used instead of obs_val if set */
   int32_t index_type;         /* LT_T_* of obs_index                                       */
   int32_t _pad;
+  /* fused load stage: when obs_bands is set, obs_val / obs_index are ignored and the value of
+   * obs o at pixel p is lin evaluated on band s = obs_bands[o*band_obs_stride + s*band_stride +
+   * p*band_pix_stride] (rast_algebra + its store, utils.py:447-484, per winner). Planar bands
+   * (lt_index_io's layout): band_pix_stride 1, band_stride >= n_pix. Pixel-interleaved bands
+   * (one pixel's n_bands values side by side): band_stride 1, band_pix_stride = n_bands — the
+   * two int16 bands of 'B1 - B2' are then one 32-bit load per winner */
+  const void* obs_bands;
+  int64_t band_obs_stride;    /* elements between the bands of consecutive obs              */
+  int64_t band_stride;        /* elements between bands of one obs at one pixel             */
+  int64_t band_pix_stride;    /* elements between consecutive pixels of one band            */
+  lt_index_lin lin;
 } lt_tile_in;
 
 /* ---- load stage: settings.json index_eqn (utils.py:447-484 rast_algebra) -------------------- */
@@ -294,6 +321,11 @@ int lt_ctx_last_deferred(lt_ctx* ctx, int64_t* n_deferred);
 int lt_index_codegen(const lt_index_prog* prog, char* buf, int64_t cap);
 int lt_index_compile(lt_ctx* ctx, const lt_index_prog* prog, lt_index** out);
 int lt_index_apply(lt_ctx* ctx, const lt_index* fn, const lt_index_io* io, void* stream);
+/* The linear form of `prog` (see lt_index_lin) for the analyze kernel's fused load stage, or
+ * LT_ERR_ARG when the program is not one (a division, a float node, a product of two band
+ * terms, mixed integer node types, a band type the kernel does not read, more than
+ * LT_LIN_MAX_BANDS bands): such programs keep lt_index_apply. Host only, no context. */
+int lt_index_linearize(const lt_index_prog* prog, lt_index_lin* out);
 
 #ifdef __cplusplus
 }

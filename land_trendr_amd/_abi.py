@@ -10,7 +10,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, 'liblt_hip.so')
 
-LT_ABI_VERSION = 3
+LT_ABI_VERSION = 4
 LT_MAX_YEARS = 64
 LT_MAX_OBS = 1024
 LT_MAX_RULES = 16
@@ -56,10 +56,22 @@ class LtScene(ctypes.Structure):
                 ('feb29_bad', c_u8p)]
 
 
+LT_LIN_MAX_BANDS = 4
+
+
+class LtIndexLin(ctypes.Structure):
+    _fields_ = [('n_bands', ctypes.c_int32), ('band_type', ctypes.c_int32),
+                ('wrap_type', ctypes.c_int32), ('out_type', ctypes.c_int32),
+                ('c0', ctypes.c_int64), ('coef', ctypes.c_int64 * LT_LIN_MAX_BANDS)]
+
+
 class LtTileIn(ctypes.Structure):
     _fields_ = [('n_pix', ctypes.c_int64), ('stride', ctypes.c_int64), ('obs_val', c_f64p),
                 ('obs_valid', c_u8p), ('obs_index', ctypes.c_void_p),
-                ('index_type', ctypes.c_int32), ('_pad', ctypes.c_int32)]
+                ('index_type', ctypes.c_int32), ('_pad', ctypes.c_int32),
+                ('obs_bands', ctypes.c_void_p), ('band_obs_stride', ctypes.c_int64),
+                ('band_stride', ctypes.c_int64), ('band_pix_stride', ctypes.c_int64),
+                ('lin', LtIndexLin)]
 
 
 class LtIndexOp(ctypes.Structure):
@@ -134,7 +146,8 @@ PIX_FIELDS = [('status', 'int32'), ('n_years', 'int32')]
 EXPORTS = ['lt_abi_version', 'lt_ctx_create', 'lt_ctx_destroy', 'lt_last_error',
            'lt_analyze_tile', 'lt_analyze_tiles', 'lt_analyze_tiles_after', 'lt_label_tile', 'lt_ctx_set_timing', 'lt_ctx_stage_ms',
            'lt_ctx_last_deferred', 'lt_index_codegen', 'lt_index_compile', 'lt_index_apply',
-           'lt_settings_compile', 'lt_raster_assemble', 'lt_winner_presence']
+           'lt_settings_compile', 'lt_raster_assemble', 'lt_winner_presence',
+           'lt_index_linearize']
 
 _LIB = None
 
@@ -174,6 +187,7 @@ def load_lib(path=None):
     lib.lt_index_codegen.restype = ctypes.c_int
     lib.lt_index_compile.argtypes = [vp, ctypes.POINTER(LtIndexProg), ctypes.POINTER(vp)]
     lib.lt_index_apply.argtypes = [vp, vp, ctypes.POINTER(LtIndexIO), vp]
+    lib.lt_index_linearize.argtypes = [ctypes.POINTER(LtIndexProg), ctypes.POINTER(LtIndexLin)]
     lib.lt_raster_assemble.argtypes = [vp, ctypes.POINTER(LtRasterJob), ctypes.c_int, vp]
     lib.lt_winner_presence.argtypes = [vp, vp, ctypes.c_int64, ctypes.c_int32, ctypes.c_int64,
                                        ctypes.c_int32, vp, vp]

@@ -297,6 +297,24 @@ static int check_tile(lt_ctx* c, const lt_tile_in* in, const lt_tile_out* out) {
   if (in->n_pix < 0 || in->stride < in->n_pix || out->stride < in->n_pix)
     return fail(c, LT_ERR_ARG, "bad n_pix/stride%s");
   if (in->n_pix == 0) return LT_OK;  // nothing is read or written
+  if (in->obs_bands) {  // the fused load stage: a linear form lt_index_linearize accepts
+    const lt_index_lin& L = in->lin;
+    if (L.n_bands < 1 || L.n_bands > LT_LIN_MAX_BANDS ||
+        (L.band_type != LT_T_I16 && L.band_type != LT_T_U16 && L.band_type != LT_T_U8 &&
+         L.band_type != LT_T_I32) ||
+        !lt_idx::is_int(L.wrap_type) || !lt_idx::ctype(L.out_type))
+      return fail(c, LT_ERR_ARG, "bad linear index form%s");
+    const bool planar = in->band_pix_stride == 1 && in->band_stride >= in->n_pix &&
+                        in->band_obs_stride >= (int64_t)L.n_bands * in->band_stride;
+    const bool interleaved = in->band_stride == 1 && in->band_pix_stride == L.n_bands &&
+                             in->band_obs_stride >= (int64_t)L.n_bands * in->n_pix;
+    if (!planar && !interleaved) return fail(c, LT_ERR_ARG, "bad band strides%s");
+    const int64_t esz = (int64_t)lt_idx::type_size(L.band_type);
+    if (interleaved && L.n_bands == 2 && esz == 2 &&
+        ((uintptr_t)in->obs_bands % 4 != 0 || in->band_obs_stride % 2 != 0))
+      return fail(c, LT_ERR_ARG, "interleaved int16 band pairs must be 4-byte aligned%s");
+    return LT_OK;
+  }
   if (!in->obs_val && !in->obs_index) return fail(c, LT_ERR_ARG, "obs_val or obs_index required%s");
   if (in->obs_index && !lt_idx::ctype(in->index_type))
     return fail(c, LT_ERR_ARG, "bad index_type%s");
@@ -648,6 +666,11 @@ int lt_index_compile(lt_ctx* c, const lt_index_prog* prog, lt_index** out) {
   c->index_fns[src] = f;
   *out = f;
   return LT_OK;
+}
+
+int lt_index_linearize(const lt_index_prog* prog, lt_index_lin* out) {
+  if (!prog || !out) return LT_ERR_ARG;
+  return lt_idx::linearize(*prog, *out) ? LT_OK : LT_ERR_ARG;
 }
 
 int lt_index_apply(lt_ctx* c, const lt_index* f, const lt_index_io* io, void* stream_) {

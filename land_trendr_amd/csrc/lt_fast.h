@@ -149,6 +149,26 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
   // years in batches of 8: the winners first, then their 8 value loads issued together (one
   // load per year in sequence would leave each wave waiting out the HBM latency 30 times)
   constexpr int WB = LT_WB;
+  // with a cloud mask of at most 128 observations, every mask byte of the pixel is loaded up
+  // front, 16 loads in flight at a time, into two bit words (bit o: obs o valid): the winner scan
+  // then tests bits instead of waiting out one dependent HBM load per observation
+  const int K = S.n_obs;
+  const bool vbits = in.obs_valid != nullptr && K <= 128;  // launch-uniform
+  uint64_t vb0 = 0, vb1 = 0;
+  if (vbits) {
+    for (int k0 = 0; k0 < K; k0 += 16) {  // wave-uniform
+      uint8_t m[16];
+#pragma unroll
+      for (int u = 0; u < 16; u++)
+        m[u] = (k0 + u < K) ? in.obs_valid[(int64_t)(k0 + u) * is + (live ? p : 0)] : 0;
+#pragma unroll
+      for (int u = 0; u < 16; u++) {
+        const uint64_t bit = (uint64_t)(m[u] != 0) << ((k0 + u) & 63);
+        if (k0 + u < 64) vb0 |= bit;
+        else vb1 |= bit;
+      }
+    }
+  }
   for (int yb = 0; yb < Y; yb += WB) {
     int best[WB];
 #pragma unroll
@@ -164,7 +184,8 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
       const int k1 = S.slot_begin[y + 1];
       for (int k = S.slot_begin[y]; k < k1; k++) {
         const int o = S.order[k];
-        const bool ok = live && in.obs_valid[(int64_t)o * is + p] != 0;
+        const bool ok = live && (vbits ? ((o < 64 ? vb0 >> o : vb1 >> (o - 64)) & 1) != 0
+                                       : in.obs_valid[(int64_t)o * is + p] != 0);
         if (ok && S.dist[k] < bd) {
           bd = S.dist[k];
           best[u] = o;
@@ -184,7 +205,73 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
 #pragma unroll
       for (int u = 0; u < WB; u++) val[u] = (double)raw[u];
     };
-    if (in.obs_index == nullptr) batch(double{});
+    // the fused load stage (lt_abi.h lt_index_lin) for int16 bands and a narrow form (node type
+    // of <= 32 bits, coefficients of 24 bits; 'B1 - B2'): the winners' band values, every load of
+    // the batch in flight at once, then 32-bit arithmetic — a multiply-add per band, one wrap, one
+    // clamp, one conversion (the sum is needed only modulo 2^bits(node type) <= 2^32). Other forms
+    // take obs_value's general path (lt_pixel.h lin_value), one value at a time: one instance of
+    // the batch keeps the kernel's code and register allocation as they are without it
+    auto fused16 = [&]() {
+      const int16_t* bb = (const int16_t*)in.obs_bands;
+      const lt_index_lin& LN = in.lin;
+      const int nb = LN.n_bands;
+      int16_t raw[LT_LIN_MAX_BANDS][WB];
+      if (nb == 2 && in.band_stride == 1) {  // a pixel-interleaved pair: one 32-bit load
+        const uint32_t* bw = (const uint32_t*)in.obs_bands;
+        const int64_t os2 = in.band_obs_stride >> 1;
+        uint32_t w[WB];
+#pragma unroll
+        for (int u = 0; u < WB; u++)
+          w[u] = bw[(int64_t)(best[u] >= 0 ? best[u] : 0) * os2 + (live ? p : 0)];
+#pragma unroll
+        for (int u = 0; u < WB; u++) {
+          raw[0][u] = (int16_t)(w[u] & 0xffffu);  // band plane 0 at the lower address
+          raw[1][u] = (int16_t)(w[u] >> 16);
+        }
+      } else {
+#pragma unroll
+        for (int s = 0; s < LT_LIN_MAX_BANDS; s++) {
+          if (s >= nb) break;  // launch-uniform
+#pragma unroll
+          for (int u = 0; u < WB; u++)
+            raw[s][u] = bb[(int64_t)(best[u] >= 0 ? best[u] : 0) * in.band_obs_stride +
+                           s * in.band_stride + (live ? p : 0) * in.band_pix_stride];
+        }
+      }
+      const int sh = 32 - lin_type_bits(LN.wrap_type);
+      const bool sgn = lin_type_signed(LN.wrap_type);
+      int64_t lo64, hi64;
+      lin_out_range(LN.out_type, lo64, hi64);
+      const int32_t lo = lo64 < INT32_MIN ? INT32_MIN : (int32_t)lo64;
+      const int32_t hi = hi64 > INT32_MAX ? INT32_MAX : (int32_t)hi64;
+#pragma unroll
+      for (int u = 0; u < WB; u++) {
+        uint32_t acc = (uint32_t)LN.c0;
+#pragma unroll
+        for (int s = 0; s < LT_LIN_MAX_BANDS; s++)
+          if (s < nb) acc += (uint32_t)__mul24((int)LN.coef[s], (int)raw[s][u]);
+        const int32_t r = sgn ? (int32_t)(acc << sh) >> sh : (int32_t)((acc << sh) >> sh);
+        if (LN.out_type == LT_T_F64) val[u] = (double)r;
+        else if (LN.out_type == LT_T_F32) val[u] = (double)(float)r;
+        else val[u] = (double)(r < lo ? lo : r > hi ? hi : r);
+      }
+    };
+    if (in.obs_bands) {
+      const lt_index_lin& LN = in.lin;
+      const int wb = lin_type_bits(LN.wrap_type);
+      bool narrow = LN.band_type == LT_T_I16 && wb <= 32 &&
+                    (wb < 32 || lin_type_signed(LN.wrap_type));
+#pragma unroll
+      for (int s = 0; s < LT_LIN_MAX_BANDS; s++)
+        if (s < LN.n_bands) narrow = narrow && LN.coef[s] >= -(1 << 23) && LN.coef[s] < (1 << 23);
+      if (narrow) {
+        fused16();
+      } else {
+#pragma unroll
+        for (int u = 0; u < WB; u++)
+          val[u] = obs_value(in, (int64_t)(best[u] >= 0 ? best[u] : 0), live ? p : 0);
+      }
+    } else if (in.obs_index == nullptr) batch(double{});
     else if (in.index_type == LT_T_I16) batch(int16_t{});
     else if (in.index_type == LT_T_F32) batch(float{});
     else if (in.index_type == LT_T_U16) batch(uint16_t{});
@@ -193,7 +280,7 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
     else {
 #pragma unroll
       for (int u = 0; u < WB; u++)
-        val[u] = obs_value(in, (int64_t)(best[u] >= 0 ? best[u] : 0) * is + (live ? p : 0));
+        val[u] = obs_value(in, (int64_t)(best[u] >= 0 ? best[u] : 0), live ? p : 0);
     }
 #pragma unroll
     for (int u = 0; u < WB; u++) {

@@ -287,4 +287,95 @@ inline std::string codegen_body(const lt_index_prog& P, bool vec, std::string& e
   return body;
 }
 
+inline bool is_int(int t) { return ctype(t) && !is_float(t); }
+
+// A program's integer linear form (lt_abi.h lt_index_lin), or false. Every arithmetic node must
+// carry the one integer type W (numpy wraps each node modulo 2^bits(W), so the whole sum taken
+// modulo 2^64 and wrapped once at the end is the same value); band operands are cast to W, which
+// must hold every band value; integer constants are cast to W by wrapping, which the modular sum
+// absorbs; a product needs a constant side; no division and no float node.
+inline bool linearize(const lt_index_prog& P, lt_index_lin& L) {
+  L = lt_index_lin{};
+  if (P.n_ops < 1 || P.n_ops > LT_MAX_PROG || P.n_bands < 1 || P.n_bands > LT_LIN_MAX_BANDS)
+    return false;
+  const int bt = P.band_type;
+  if (bt != LT_T_I16 && bt != LT_T_U16 && bt != LT_T_U8 && bt != LT_T_I32) return false;
+  if (!ctype(P.out_type)) return false;
+  struct Form {
+    bool band;  // some coefficient may be non-zero (a band term)
+    uint64_t c0, c[LT_LIN_MAX_BANDS];
+  };
+  std::vector<Form> st;
+  int W = -1;
+  // a band of type bt cast to W keeps its value
+  auto holds = [&](int w) {
+    long long blo, bhi, wlo, whi;
+    int_range(bt, blo, bhi);
+    int_range(w, wlo, whi);
+    if (w == LT_T_U32 && bt == LT_T_I32) return false;
+    return blo >= wlo && bhi <= whi;
+  };
+  for (int k = 0; k < P.n_ops; k++) {
+    const lt_index_op& o = P.ops[k];
+    Form f{};
+    switch (o.op) {
+      case LT_OP_BAND:
+        if (o.ival < 0 || o.ival >= P.n_bands || o.type != bt) return false;
+        f.band = true;
+        f.c[o.ival] = 1;
+        st.push_back(f);
+        continue;
+      case LT_OP_CONST_I:
+        f.c0 = (uint64_t)o.ival;
+        st.push_back(f);
+        continue;
+      case LT_OP_ADD:
+      case LT_OP_SUB:
+      case LT_OP_MUL:
+      case LT_OP_NEG:
+        break;
+      default:  // a float constant, a division
+        return false;
+    }
+    if (!is_int(o.type) || (W >= 0 && o.type != W)) return false;
+    W = o.type;
+    if (o.op == LT_OP_NEG) {
+      if (st.empty()) return false;
+      Form& a = st.back();
+      a.c0 = 0 - a.c0;
+      for (int s = 0; s < LT_LIN_MAX_BANDS; s++) a.c[s] = 0 - a.c[s];
+      continue;
+    }
+    if (st.size() < 2) return false;
+    const Form b = st.back();
+    st.pop_back();
+    Form& a = st.back();
+    if (o.op == LT_OP_MUL) {
+      if (a.band && b.band) return false;  // a product of two band terms
+      const Form& cst = a.band ? b : a;
+      const Form& var = a.band ? a : b;
+      Form r{};
+      r.band = var.band;
+      r.c0 = var.c0 * cst.c0;
+      for (int s = 0; s < LT_LIN_MAX_BANDS; s++) r.c[s] = var.c[s] * cst.c0;
+      a = r;
+    } else {
+      const bool sub = o.op == LT_OP_SUB;
+      a.band = a.band || b.band;
+      a.c0 = sub ? a.c0 - b.c0 : a.c0 + b.c0;
+      for (int s = 0; s < LT_LIN_MAX_BANDS; s++) a.c[s] = sub ? a.c[s] - b.c[s] : a.c[s] + b.c[s];
+    }
+  }
+  if (st.size() != 1) return false;
+  if (W < 0) W = bt;  // the program is one band plane: its values, stored into out_type
+  if (!holds(W)) return false;
+  L.n_bands = P.n_bands;
+  L.band_type = bt;
+  L.wrap_type = W;
+  L.out_type = P.out_type;
+  L.c0 = (int64_t)st[0].c0;
+  for (int s = 0; s < LT_LIN_MAX_BANDS; s++) L.coef[s] = (int64_t)st[0].c[s];
+  return true;
+}
+
 }  // namespace lt_idx

@@ -232,9 +232,72 @@ struct RuleState {
 // difference within 2^-49.5 (the test requires 2^-40): 2^-30 leaves a margin of at least 2^10.
 constexpr double kScreen = 0x1p-30;
 
-// Observation value i of a tile: the f64 values, or the index raster in its stored type
-// (float(val), utils.py:357). index_type is uniform over a launch: a scalar branch on the GPU.
-__host__ __device__ inline double obs_value(const lt_tile_in& in, int64_t i) {
+// The fused load stage (lt_abi.h lt_index_lin): the index value of the band values whose
+// linear form is acc (modulo 2^64), as lt_index_apply would store it into out_type and the analyze
+// stage read it back (float(val), utils.py:357): wrapped to the node type, then the store into
+// out_type (lt_index.h codegen: saturation into an integer type, rounding into binary32).
+__host__ __device__ inline int lin_type_bits(int t) {
+  switch (t) {
+    case LT_T_I8: case LT_T_U8: return 8;
+    case LT_T_I16: case LT_T_U16: return 16;
+    case LT_T_I32: case LT_T_U32: return 32;
+    default: return 64;
+  }
+}
+__host__ __device__ inline bool lin_type_signed(int t) {
+  return t == LT_T_I8 || t == LT_T_I16 || t == LT_T_I32 || t == LT_T_I64;
+}
+__host__ __device__ inline void lin_out_range(int t, int64_t& lo, int64_t& hi) {
+  const int b = lin_type_bits(t);
+  if (b == 64) {  // I64 (a U64 store type does not exist)
+    lo = (int64_t)(1ull << 63);
+    hi = (int64_t)((1ull << 63) - 1);
+  } else if (lin_type_signed(t)) {
+    lo = -(int64_t)(1ull << (b - 1));
+    hi = (int64_t)(1ull << (b - 1)) - 1;
+  } else {
+    lo = 0;
+    hi = (int64_t)((1ull << b) - 1);
+  }
+}
+__host__ __device__ inline double lin_store(const lt_index_lin& L, uint64_t acc) {
+  const int bits = lin_type_bits(L.wrap_type);
+  int64_t r = (int64_t)acc;
+  if (bits < 64) {
+    const int sh = 64 - bits;
+    r = lin_type_signed(L.wrap_type) ? (int64_t)(acc << sh) >> sh : (int64_t)((acc << sh) >> sh);
+  }
+  if (L.out_type == LT_T_F64) return (double)r;
+  if (L.out_type == LT_T_F32) return (double)(float)r;
+  int64_t lo, hi;
+  lin_out_range(L.out_type, lo, hi);
+  return (double)(r < lo ? lo : r > hi ? hi : r);
+}
+template <class B>
+__host__ __device__ inline uint64_t lin_term(int64_t coef, B b) {
+  return (uint64_t)coef * (uint64_t)(int64_t)b;
+}
+__host__ __device__ inline double lin_value(const lt_tile_in& in, int64_t o, int64_t p) {
+  const lt_index_lin& L = in.lin;
+  uint64_t acc = (uint64_t)L.c0;
+  for (int s = 0; s < L.n_bands && s < LT_LIN_MAX_BANDS; s++) {
+    const int64_t i = o * in.band_obs_stride + s * in.band_stride + p * in.band_pix_stride;
+    switch (L.band_type) {
+      case LT_T_I16: acc += lin_term(L.coef[s], ((const int16_t*)in.obs_bands)[i]); break;
+      case LT_T_U16: acc += lin_term(L.coef[s], ((const uint16_t*)in.obs_bands)[i]); break;
+      case LT_T_U8: acc += lin_term(L.coef[s], ((const uint8_t*)in.obs_bands)[i]); break;
+      default: acc += lin_term(L.coef[s], ((const int32_t*)in.obs_bands)[i]); break;
+    }
+  }
+  return lin_store(L, acc);
+}
+
+// Value of observation o at pixel p of a tile: the f64 values, the index raster in its stored
+// type (float(val), utils.py:357), or the fused load stage's value from the band planes.
+// index_type is uniform over a launch: a scalar branch on the GPU.
+__host__ __device__ inline double obs_value(const lt_tile_in& in, int64_t o, int64_t p) {
+  if (in.obs_bands) return lin_value(in, o, p);
+  const int64_t i = o * in.stride + p;
   if (in.obs_index == nullptr) return in.obs_val[i];
   switch (in.index_type) {
     case LT_T_I16: return (double)((const int16_t*)in.obs_index)[i];
@@ -534,7 +597,7 @@ __host__ __device__ bool analyze_pixel(const DevScene& S, const lt_params& P, co
     if (out.winner) out.winner[(int64_t)y * os + p] = (int16_t)best;
     if (best >= 0) {
       if ((S.feb29_mask >> y) & 1) status |= LT_ST_FEB29;
-      val[T] = obs_value(in, (int64_t)best * is + p);
+      val[T] = obs_value(in, (int64_t)best, p);
       slot[T] = (uint8_t)y;
       T++;
     }

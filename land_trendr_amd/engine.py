@@ -71,12 +71,13 @@ class Engine:
         return out
 
     def analyze_tile(self, scene, params, values, valid=None, fields=ALL_FIELDS, out=None,
-                     stream=None):
+                     stream=None, lin=None):
         """values: [K, P] observation values — float64, or an index raster in its stored type
         (int16, uint16, int32, float32, uint8, ...: what index_tile writes) — valid: uint8 [K, P]
-        or None. Returns the dict of output tensors ([Y, P], [R, P], [P]); asynchronous on
-        `stream`."""
-        tin, tout, out = self._tile_structs(scene, params, values, valid, fields, out)
+        or None. With lin (an IndexFn's linear form, fn.lin): values are the [K, NB, P] band
+        planes and the kernel evaluates the index of each winner itself (the fused load stage).
+        Returns the dict of output tensors ([Y, P], [R, P], [P]); asynchronous on `stream`."""
+        tin, tout, out = self._tile_structs(scene, params, values, valid, fields, out, lin)
         sc = scene.to_c()
         st = stream if stream is not None else torch.cuda.current_stream(self.device)
         rc = self.lib.lt_analyze_tile(self.ctx, ctypes.byref(sc), ctypes.byref(params),
@@ -86,19 +87,20 @@ class Engine:
         return out
 
     def analyze_tiles(self, scene, params, tiles, fields=ALL_FIELDS, outs=None, stream=None,
-                      ready=None):
+                      ready=None, lin=None):
         """analyze_tile over a list of (values, valid) tiles of one scene in one call
         (lt_analyze_tiles: tile t's resolve stage overlaps tile t+1's analyze stage). ready: None
         or one recorded torch.cuda.Event (or None) per tile, which that tile's analyze kernel
         waits on (lt_analyze_tiles_after: the load stage of later tiles may still be running on
-        another stream). Returns the list of output dicts; asynchronous on `stream`."""
+        another stream). lin: as analyze_tile (every tile's values are then band planes).
+        Returns the list of output dicts; asynchronous on `stream`."""
         n = len(tiles)
         tins = (_abi.LtTileIn * max(n, 1))()
         touts = (_abi.LtTileOut * max(n, 1))()
         res = []
         for t, (values, valid) in enumerate(tiles):
             tin, tout, o = self._tile_structs(scene, params, values, valid, fields,
-                                              outs[t] if outs is not None else None)
+                                              outs[t] if outs is not None else None, lin)
             tins[t] = tin
             touts[t] = tout
             res.append(o)
@@ -118,16 +120,31 @@ class Engine:
         self._check(rc, 'lt_analyze_tiles')
         return res
 
-    def _tile_structs(self, scene, params, values, valid, fields, out):
-        if values.dtype not in _LT_T or values.device != self.device or values.dim() != 2:
-            raise LtError('values must be a [K, P] raster tensor on %s' % self.device)
-        if values.stride(1) != 1:
-            raise LtError('values must have unit pixel stride')
-        K, P = values.shape
+    def _tile_structs(self, scene, params, values, valid, fields, out, lin=None):
+        if lin is not None:  # the fused load stage: [K, NB, P] band planes
+            want = _TORCH_OF_LT.get(lin.band_type)
+            planar = values.dim() == 3 and values.stride(2) == 1
+            inter = values.dim() == 3 and values.stride(1) == 1 and values.stride(2) == lin.n_bands
+            if (values.dtype != want or values.device != self.device or values.dim() != 3 or
+                    values.shape[1] != lin.n_bands or not (planar or inter)):
+                raise LtError('bands must be a %s [K, %d, P] tensor on %s, planar (unit pixel '
+                              'stride) or pixel-interleaved (unit band stride)'
+                              % (want, lin.n_bands, self.device))
+            K, _, P = values.shape
+        else:
+            if values.dtype not in _LT_T or values.device != self.device or values.dim() != 2:
+                raise LtError('values must be a [K, P] raster tensor on %s' % self.device)
+            if values.stride(1) != 1:
+                raise LtError('values must have unit pixel stride')
+            K, P = values.shape
         if K != scene.n_obs:
             raise LtError('values has %d obs rows, scene has %d' % (K, scene.n_obs))
         if valid is not None:
-            if (valid.dtype != torch.uint8 or valid.shape != values.shape or
+            if lin is not None:
+                if (valid.dtype != torch.uint8 or tuple(valid.shape) != (K, P) or
+                        valid.stride(1) != 1 or valid.device != self.device):
+                    raise LtError('valid must be a uint8 [K, P] tensor with unit pixel stride')
+            elif (valid.dtype != torch.uint8 or valid.shape != values.shape or
                     valid.stride() != values.stride() or valid.device != self.device):
                 raise LtError('valid must be uint8 with the shape/strides of values')
         if out is None:
@@ -148,10 +165,18 @@ class Engine:
                     raise LtError('all [Y|R, P] outputs must share one row stride')
         tin = _abi.LtTileIn()
         tin.n_pix = P
-        tin.stride = values.stride(0)
-        if values.dtype == torch.float64:
+        if lin is not None:
+            tin.stride = valid.stride(0) if valid is not None else P
+            tin.obs_bands = values.data_ptr()
+            tin.band_obs_stride = values.stride(0)
+            tin.band_stride = values.stride(1)
+            tin.band_pix_stride = values.stride(2)
+            tin.lin = lin
+        elif values.dtype == torch.float64:
+            tin.stride = values.stride(0)
             tin.obs_val = ctypes.cast(values.data_ptr(), _abi.c_f64p)
         else:
+            tin.stride = values.stride(0)
             tin.obs_index = values.data_ptr()
             tin.index_type = _LT_T[values.dtype]
         tin.obs_valid = ctypes.cast(valid.data_ptr(), _abi.c_u8p) if valid is not None else None
@@ -169,7 +194,7 @@ class Engine:
         with torch.cuda.device(self.device):
             self._check(self.lib.lt_index_compile(self.ctx, ctypes.byref(prog), ctypes.byref(fn)),
                         'lt_index_compile')
-        return IndexFn(fn, program)
+        return IndexFn(fn, program, linear_form(program))
 
     def index_tile(self, fn, bands, out=None, stream=None):
         """bands: [K, NB, P] band planes (NB = the program's band slots, unit pixel stride) in
@@ -180,8 +205,10 @@ class Engine:
             raise LtError('bands must be a %s [K, %d, P] tensor on %s' % (want, len(prog.bands),
                                                                          self.device))
         K, NB, P = bands.shape
-        if NB != len(prog.bands) or bands.stride(2) != 1:
-            raise LtError('bands must have %d band planes and unit pixel stride' % len(prog.bands))
+        if NB != len(prog.bands):
+            raise LtError('bands must have %d band planes' % len(prog.bands))
+        if bands.stride(2) != 1:  # pixel-interleaved bands: the load kernel reads planes
+            bands = bands.contiguous()
         odt = _TORCH_OF_LT[_LT_T_OF_NP(prog.out_dtype)]
         if out is None:
             out = torch.empty((K, P), dtype=odt, device=self.device)
@@ -226,11 +253,27 @@ class Engine:
 
 
 class IndexFn:
-    """A compiled load-stage kernel (owned by the engine's context)."""
+    """A compiled load-stage kernel (owned by the engine's context). lin: the program's integer
+    linear form (_abi.LtIndexLin) when it has one: the analyze kernel then evaluates the index of
+    each winner from the band planes itself (analyze_tile(..., lin=fn.lin)), and the load kernel
+    is needed only to materialise an index raster."""
 
-    def __init__(self, handle, program):
+    def __init__(self, handle, program, lin=None):
         self.handle = handle
         self.program = program
+        self.lin = lin
+
+
+def linear_form(program):
+    """lt_index_linearize of an index_eqn.IndexProgram: its _abi.LtIndexLin, or None when the
+    program is not an integer linear form (divisions, float nodes, products of band terms, mixed
+    node types, more than LT_LIN_MAX_BANDS bands). Host-only: needs the library, not a GPU."""
+    lib = _abi.load_lib()
+    lin = _abi.LtIndexLin()
+    prog = program.to_c()
+    if lib.lt_index_linearize(ctypes.byref(prog), ctypes.byref(lin)) != 0:
+        return None
+    return lin
 
 
 def _LT_T_OF_NP(np_dtype):

@@ -2,8 +2,11 @@
 
 For every tile this rank owns (distributed.Mosaic), in tile order:
   1. load stage (parse_mapper's rast_algebra, mr_land_trendr_job.py:67-68 / utils.py:447-484):
-     the hiprtc-compiled index_eqn kernel turns the tile's band planes into its index raster, on a
-     stream of its own, recording an event per tile;
+     when the index_eqn program is an integer linear form (engine.IndexFn.lin; 'B1 - B2' is one)
+     the analyze kernel evaluates it on the winners' band values itself (the fused load stage: no
+     index raster, no kernel between tiles); otherwise the hiprtc-compiled index_eqn kernel turns
+     the tile's band planes into its index raster, on a stream of its own, recording an event per
+     tile;
   2. analyze + label (analysis_reducer, mr_land_trendr_job.py:83-126): lt_analyze_tiles_after on
      the current stream, tile t waiting only for tile t's index event, so later tiles' load
      kernels (HBM-bound) run beside earlier tiles' analyze kernels (issue-bound); consecutive
@@ -44,7 +47,8 @@ class MosaicRunner:
     scene, or 1 when labels are exchanged, so tile t's sends travel while tile t+1 computes)."""
 
     def __init__(self, engine, mosaic, params, items, fields, index_fn=None, dist=None,
-                 exchange_fields=LABEL_GATHER_FIELDS, load_stream=True, group=0, dst=0):
+                 exchange_fields=LABEL_GATHER_FIELDS, load_stream=True, group=0, dst=0,
+                 fused=None):
         self.eng, self.m, self.params, self.items = engine, mosaic, params, list(items)
         self.fields = tuple(fields)
         self.index_fn = index_fn
@@ -78,9 +82,17 @@ class MosaicRunner:
             raise ValueError('band inputs need a compiled index_eqn (index_fn)')
         # (a CPU engine — the gloo tests' oracle double — has no streams: everything is serial)
         self.cuda = torch.device(engine.device).type == 'cuda'
+        # fused load stage (engine.IndexFn.lin): on unless fused=False or LT_FUSED_INDEX=0
+        if fused is None:
+            fused = os.environ.get('LT_FUSED_INDEX', '1') != '0'
+        self.lin = (getattr(index_fn, 'lin', None)
+                    if fused and has_bands and all(it.bands is not None for it in self.items)
+                    else None)
+        self.fused = self.lin is not None
         prio = int(os.environ.get('LT_LOAD_PRIORITY', '0'))
         self.load_stream = (torch.cuda.Stream(engine.device, priority=prio)
-                            if self.cuda and has_bands and load_stream else None)
+                            if self.cuda and has_bands and load_stream and not self.fused
+                            else None)
         self.index_events = []  # (start, stop) pairs of the timed steps' load kernels
 
     def _groups(self):
@@ -103,6 +115,8 @@ class MosaicRunner:
         eng = self.eng
         if not self.cuda:
             timed = False
+        if self.fused:
+            return self._step_fused(after_tile, stage_in)
         main = torch.cuda.current_stream(eng.device) if self.cuda else None
         ready = [None] * len(self.items)
         if self.load_stream is not None:  # the previous step's analyze kernels read the rasters
@@ -149,6 +163,47 @@ class MosaicRunner:
         for k in range(len(self.items), self.m.rounds):
             self.exchange.post(k)
         self.exchange.wait()
+
+    def _step_fused(self, after_tile, stage_in):
+        """step() with the fused load stage: each tile's analyze kernel reads its band planes.
+        With stage_in, one tile per call: tile k's analyze waits for its H2D copy, and its slab is
+        handed back once the call's work (analyze + resolve) is done."""
+        eng = self.eng
+        main = torch.cuda.current_stream(eng.device)
+        groups = ([[k] for k in range(len(self.items))] if stage_in is not None
+                  else list(self._groups()))
+        for g in groups:
+            scene = self.items[g[0]].scene
+            n = [self.items[k].tile.n for k in g]
+            tiles, ready = [], None
+            for k in g:
+                bands = self.items[k].bands
+                if stage_in is not None:
+                    bands, ev_in = stage_in.fetch(k)
+                    ready = [ev_in]
+                tiles.append((bands, self.items[k].valid))
+            eng.analyze_tiles(
+                scene, self.params, tiles, self.fields,
+                outs=[{f: x[..., :nk] for f, x in self.outs[k].items()} for k, nk in zip(g, n)],
+                ready=ready, lin=self.lin)
+            if stage_in is not None:
+                ev = torch.cuda.Event()
+                ev.record(main)
+                stage_in.consumed(g[0], ev)
+            for k in g:
+                self.exchange.post(k)
+                if after_tile is not None:
+                    after_tile(k)
+        for k in range(len(self.items), self.m.rounds):
+            self.exchange.post(k)
+        self.exchange.wait()
+
+    def materialise_index(self, k):
+        """Tile k's index raster (items[k].values) from its band planes with the load kernel, on
+        the current stream — what the fused steps never write; the oracle checks read it."""
+        if self.index_fn is None or self.items[k].bands is None:
+            return
+        self.eng.index_tile(self.index_fn, self.items[k].bands, out=self.items[k].values)
 
     def index_ms(self):
         ev, self.index_events = self.index_events, []

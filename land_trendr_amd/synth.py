@@ -39,8 +39,11 @@ class Scene:
 
 
 def make_scene(n_pix, n_years=30, k_min=1, k_max=1, mask_prob=0.0, first_year=1985, seed=0,
-               device='cpu', with_bands=False, spike_prob=0.05, chunk=1 << 22):
-    """Build a seeded synthetic scene. Deterministic for a given (seed, device type)."""
+               device='cpu', with_bands=False, spike_prob=0.05, chunk=1 << 22,
+               band_layout='planar'):
+    """Build a seeded synthetic scene. Deterministic for a given (seed, device type).
+    band_layout: 'planar' ([K, 2, P] contiguous) or 'pixel' (the same [K, 2, P] view of a
+    [K, P, 2] buffer: each pixel's two bands side by side, the fused load stage's layout)."""
     g_cpu = torch.Generator().manual_seed(int(seed))
     # --- per-scene observation dates (obs order = ascending acquisition date) ---
     dates = []
@@ -57,7 +60,11 @@ def make_scene(n_pix, n_years=30, k_min=1, k_max=1, mask_prob=0.0, first_year=19
     t_obs = torch.tensor(year_of_obs, dtype=torch.int32, device=dev)
     values = torch.empty((K, n_pix), dtype=torch.float64, device=dev)
     valid = torch.empty((K, n_pix), dtype=torch.uint8, device=dev) if mask_prob > 0 else None
-    bands = torch.empty((K, 2, n_pix), dtype=torch.int16, device=dev) if with_bands else None
+    bands = None
+    if with_bands:
+        bands = (torch.empty((K, n_pix, 2), dtype=torch.int16, device=dev).permute(0, 2, 1)
+                 if band_layout == 'pixel' else
+                 torch.empty((K, 2, n_pix), dtype=torch.int16, device=dev))
     for p0 in range(0, n_pix, chunk):
         p1 = min(n_pix, p0 + chunk)
         n = p1 - p0
@@ -90,18 +97,20 @@ def make_scene(n_pix, n_years=30, k_min=1, k_max=1, mask_prob=0.0, first_year=19
 
 
 def mosaic_inputs(mosaic, n_years, k_min=1, k_max=1, mask_prob=0.0, seed0=1000, device='cpu',
-                  target_date='2014-07-01'):
+                  target_date='2014-07-01', band_layout='pixel'):
     """runner.TileInput for every tile this rank owns in `mosaic`: scene s is the seeded scene
     make_scene(seed=seed0 + s) as int16 bands (B1, B2) + cloud mask, so a tile's content does not
     depend on the number of ranks. A rank owning a whole scene keeps it in place (tiles are views
-    sharing one index raster); otherwise its tiles are copied out and the scene freed."""
+    sharing one index raster); otherwise its tiles are copied out and the scene freed. Bands are
+    pixel-interleaved by default (make_scene band_layout)."""
     from .runner import TileInput
     from .scene import build_scene, parse_date
     items = []
     dev = torch.device(device)
     for s in sorted({t.scene for t in mosaic.mine}):
         sc = make_scene(mosaic.scene_pixels[s], n_years=n_years, k_min=k_min, k_max=k_max,
-                        mask_prob=mask_prob, seed=seed0 + s, device=dev, with_bands=True)
+                        mask_prob=mask_prob, seed=seed0 + s, device=dev, with_bands=True,
+                        band_layout=band_layout)
         sc.values = None  # only the bands travel (the load stage computes the index raster)
         meta = build_scene(sc.dates, parse_date(target_date))
         mine = [t for t in mosaic.mine if t.scene == s]

@@ -67,6 +67,8 @@ def main():
     fn = eng.compile_index(IndexProgram('B1 - B2', band_dtype='int16'))
     runner = MosaicRunner(eng, m, params, items, fields, fn)
     runner.step()
+    for k in range(len(items)):  # the fused steps read the bands: the oracle reads their raster
+        runner.materialise_index(k)
     torch.cuda.synchronize()
     print('gpu done: %d px in %d tiles, %.1f s' % (P, len(items), time.time() - t0), flush=True)
     threads = args.threads or min(len(os.sched_getaffinity(0)), 64)

@@ -174,3 +174,50 @@ def test_load_stage_on_own_stream_with_ready_events(engine):
                 continue  # unmatched slots hold no defined value
             same = _bits_equal(want[f][..., a:b], x)
             assert same.all(), (a, b, f, int((~same).sum()))
+
+
+FUSED = [('B1 - B2', np.int16, None), ('B1 * 300 - B2 * 300', np.int16, None),
+         ('-(B1 - 2 * B3) + 30000', np.int16, None), ('B1 - B2', np.uint16, np.int16),
+         ('(B2 - B1) * 2', np.uint16, None), ('B1 + B2 - 100', np.uint8, None),
+         ('3 * B1 - B2', np.int32, None), ('B1 - B2', np.int16, np.float32),
+         ('B1 + 70000 - B2', np.int16, np.int16), ('B1 + 2 - B2 + B3 - B4', np.int16, None)]
+
+
+@pytest.mark.parametrize('eqn,bt,ot', FUSED)
+@pytest.mark.parametrize('masked', [False, True])
+def test_fused_load_stage_matches_index_raster_path(engine, eqn, bt, ot, masked):
+    """The analyze kernel evaluating a linear index_eqn on the winners' band values (lt_tile_in
+    obs_bands + lt_index_lin) writes exactly what it writes from the load kernel's index raster
+    of the same bands, in every output plane (wrapping and saturating values included)."""
+    from land_trendr_amd.engine import ALL_FIELDS
+    prog = index_eqn.IndexProgram(eqn, band_dtype=bt, out_dtype=ot)
+    fn = engine.compile_index(prog)
+    assert fn.lin is not None
+    rng = np.random.default_rng(zlib.crc32((eqn + str(bt) + str(masked)).encode()))
+    Y, P = 30, 6000
+    k_per = rng.integers(1, 4, Y) if masked else np.ones(Y, int)
+    dates = []
+    for y in range(Y):
+        for _ in range(k_per[y]):
+            dates.append('%d-%02d-%02d' % (1990 + y, rng.integers(5, 10), rng.integers(1, 28)))
+    K = len(dates)
+    meta = build_scene(dates, parse_date('2014-07-01'))
+    info = np.iinfo(np.dtype(bt))
+    lo, hi = max(int(info.min), -3000), min(int(info.max), 3000)
+    base = rng.integers(lo, hi + 1, (1, len(prog.bands), P))
+    b = np.clip(base + rng.integers(-400, 401, (K, len(prog.bands), P)), info.min, info.max)
+    b[:, :, :16] = rng.integers(info.min, int(info.max) + 1, (K, len(prog.bands), 16))  # extremes
+    bands = torch.from_numpy(b.astype(bt)).to(engine.device)
+    valid = None
+    if masked:
+        valid = torch.from_numpy((rng.random((K, P)) > 0.2).astype(np.uint8)).to(engine.device)
+    params, _ = compile_params(1.0, [{'name': 'gd', 'val': 1, 'change_type': 'GD'},
+                                     {'name': 'fd', 'val': 2, 'change_type': 'FD'}])
+    idx = engine.index_tile(fn, bands)
+    want = engine.analyze_tile(meta, params, idx, valid, ALL_FIELDS)
+    got = engine.analyze_tile(meta, params, bands, valid, ALL_FIELDS, lin=fn.lin)
+    torch.cuda.synchronize()
+    for f in ALL_FIELDS:
+        w, g = want[f].cpu().numpy(), got[f].cpu().numpy()
+        same = _bits_equal(w, g)
+        assert same.all(), '%s %s: %s differs in %d places' % (eqn, bt, f, (~same).sum())

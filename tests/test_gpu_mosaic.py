@@ -1,8 +1,9 @@
 """The bench / job code path on the GPU at BASELINE.json sizes: synthetic int16 band stacks
-(synth.mosaic_inputs, bench.py's seeds and tiling) -> index_eqn 'B1 - B2' on the load stream ->
-lt_analyze_tiles_after -> label exchange (runner.MosaicRunner), checked against the CPU oracle on
-200,000 sampled pixels per config (fed the index raster the load kernel wrote, as the reference's
-apply_grid feeds float(val) of the rast_algebra raster), plus whole-raster invariants. c4 is the
+(synth.mosaic_inputs, bench.py's seeds and tiling) -> index_eqn 'B1 - B2' (fused into the analyze
+kernel: a linear form) -> lt_analyze_tiles -> label exchange (runner.MosaicRunner), checked
+against the CPU oracle on 200,000 sampled pixels per config (fed the index raster the load kernel
+writes from the same bands, as the reference's apply_grid feeds float(val) of the rast_algebra
+raster), plus whole-raster invariants. c4 is the
 4-scene, 196 Mpx mosaic of configs[3], dealt round-robin in 6.1 Mpx tiles as bench.py deals it
 (one rank here: every tile of the mosaic on this GPU)."""
 import os
@@ -75,7 +76,10 @@ def test_bench_path_full_size_sampled_vs_oracle(cfg):
             mt = o['matched'].bool()
             assert bool(((o['class_val'] != -99) == mt).all())
             assert bool(((o['duration'] > 0) | ~mt).all())
-            # the load stage: the index raster is B1 - B2 of the tile's int16 bands
+            # the load stage: the index raster is B1 - B2 of the tile's int16 bands (the fused
+            # steps never write it: the load kernel materialises it for the oracle)
+            assert runner.fused
+            runner.materialise_index(k)
             b = it.bands
             assert torch.equal(it.values, (b[:, 0, :].int() - b[:, 1, :].int()).short())
         n = SAMPLE // len(m.scene_pixels)

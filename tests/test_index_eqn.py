@@ -119,3 +119,61 @@ def test_geotiff_reader_fixture_metadata():
     assert (g.width, g.height, g.bands) == (54, 45, 1)
     assert g.pixel_scale[:2] == (30.0, 30.0)
     assert g.width * g.height == 2430  # utils_test.py:130 test_grid count
+
+
+# ---- the fused load stage: lt_index_linearize (lt_index.h) ----------------------------------
+
+def _lin_eval(lin, bands):
+    """The linear form's value as the analyze kernel computes it (lt_pixel.h lin_value /
+    lt_fast.h's fused batch): the sum modulo 2^64, the wrap to the node type, the store."""
+    M = 1 << 64
+    acc = np.full(bands.shape[1:], lin.c0 % M, dtype=object)
+    for s in range(lin.n_bands):
+        acc = (acc + (lin.coef[s] % M) * bands[s].astype(np.int64).astype(object)) % M
+    w = np.dtype(index_eqn.CODES[lin.wrap_type])
+    bits = w.itemsize * 8
+    r = acc % (1 << bits)
+    if w.kind == 'i':
+        r = np.where(r >= 1 << (bits - 1), r - (1 << bits), r)
+    out = np.dtype(index_eqn.CODES[lin.out_type])
+    if out.kind == 'f':
+        return np.array([out.type(int(v)) for v in r.ravel()], out).reshape(r.shape)
+    info = np.iinfo(out)
+    return np.clip(r, info.min, info.max).astype(out)
+
+
+LINEAR = [('B1 - B2', 'int16', None), ('B1 + B2 * 3 - 7', 'int16', None),
+          ('B1 * 300 - B2 * 300', 'int16', None), ('-(B1 - 2 * B3) + 30000', 'int16', None),
+          ('(B2 - B1) * 2', 'uint16', None), ('B1 - B2', 'uint16', 'int16'),
+          ('B1 + B2 - 100', 'uint8', None), ('3 * B1 - B2', 'int32', None),
+          ('B1 - B2', 'int16', 'float32'), ('B1 + 70000 - B2', 'int16', 'int16'),
+          ('B1', 'int16', None), ('B1 * -1', 'uint8', 'int16'), ('B1 + 2 - B2 + B3 - B4', 'int16', None)]
+NONLINEAR = [('B1 * B2', 'int16'), ('B1 / 2', 'int16'), ('B1 // B2', 'int16'),
+             ('B1 - B2 + 0.5', 'int16'), ('(B1 - B2) + 40000', 'int16'), ('B1 - B2', 'float32'),
+             ('B1 + B2 + B3 + B4 + B5', 'int16'), ('B1 - B2', 'int8'),
+             ('-(B1 - 2 * B3) + 40000', 'int16')]
+
+
+@pytest.mark.parametrize('eqn,bt,ot', LINEAR)
+def test_linear_form_matches_numpy_evaluation(eqn, bt, ot):
+    """Every program lt_index_linearize accepts gives, through its form, exactly what the numpy
+    restatement of rast_algebra + its store gives (wrapping and saturating values included)."""
+    from land_trendr_amd.engine import linear_form
+    prog = index_eqn.IndexProgram(eqn, band_dtype=bt, out_dtype=ot)
+    lin = linear_form(prog)
+    assert lin is not None, eqn
+    rng = np.random.default_rng(7)
+    info = np.iinfo(np.dtype(bt))
+    b = rng.integers(info.min, int(info.max) + 1, size=(len(prog.bands), 4000)).astype(bt)
+    b[:, :8] = info.min
+    b[:, 8:16] = info.max
+    want = index_oracle.evaluate(prog, b)
+    got = _lin_eval(lin, b)
+    assert got.dtype == want.dtype
+    np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.parametrize('eqn,bt', NONLINEAR)
+def test_nonlinear_programs_keep_the_load_kernel(eqn, bt):
+    from land_trendr_amd.engine import linear_form
+    assert linear_form(index_eqn.IndexProgram(eqn, band_dtype=bt)) is None
