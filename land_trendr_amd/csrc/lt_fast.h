@@ -149,26 +149,6 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
   // years in batches of 8: the winners first, then their 8 value loads issued together (one
   // load per year in sequence would leave each wave waiting out the HBM latency 30 times)
   constexpr int WB = LT_WB;
-  // with a cloud mask of at most 128 observations, every mask byte of the pixel is loaded up
-  // front, 16 loads in flight at a time, into two bit words (bit o: obs o valid): the winner scan
-  // then tests bits instead of waiting out one dependent HBM load per observation
-  const int K = S.n_obs;
-  const bool vbits = in.obs_valid != nullptr && K <= 128;  // launch-uniform
-  uint64_t vb0 = 0, vb1 = 0;
-  if (vbits) {
-    for (int k0 = 0; k0 < K; k0 += 16) {  // wave-uniform
-      uint8_t m[16];
-#pragma unroll
-      for (int u = 0; u < 16; u++)
-        m[u] = (k0 + u < K) ? in.obs_valid[(int64_t)(k0 + u) * is + (live ? p : 0)] : 0;
-#pragma unroll
-      for (int u = 0; u < 16; u++) {
-        const uint64_t bit = (uint64_t)(m[u] != 0) << ((k0 + u) & 63);
-        if (k0 + u < 64) vb0 |= bit;
-        else vb1 |= bit;
-      }
-    }
-  }
   for (int yb = 0; yb < Y; yb += WB) {
     int best[WB];
 #pragma unroll
@@ -184,8 +164,7 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
       const int k1 = S.slot_begin[y + 1];
       for (int k = S.slot_begin[y]; k < k1; k++) {
         const int o = S.order[k];
-        const bool ok = live && (vbits ? ((o < 64 ? vb0 >> o : vb1 >> (o - 64)) & 1) != 0
-                                       : in.obs_valid[(int64_t)o * is + p] != 0);
+        const bool ok = live && in.obs_valid[(int64_t)o * is + p] != 0;
         if (ok && S.dist[k] < bd) {
           bd = S.dist[k];
           best[u] = o;
@@ -215,18 +194,19 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
       const int16_t* bb = (const int16_t*)in.obs_bands;
       const lt_index_lin& LN = in.lin;
       const int nb = LN.n_bands;
-      int16_t raw[LT_LIN_MAX_BANDS][WB];
+      int32_t raw[LT_LIN_MAX_BANDS][WB];  // sign-extended band values
       if (nb == 2 && in.band_stride == 1) {  // a pixel-interleaved pair: one 32-bit load
-        const uint32_t* bw = (const uint32_t*)in.obs_bands;
+        const int32_t* bw = (const int32_t*)in.obs_bands;
         const int64_t os2 = in.band_obs_stride >> 1;
-        uint32_t w[WB];
+        int32_t w[WB];
 #pragma unroll
         for (int u = 0; u < WB; u++)
           w[u] = bw[(int64_t)(best[u] >= 0 ? best[u] : 0) * os2 + (live ? p : 0)];
 #pragma unroll
         for (int u = 0; u < WB; u++) {
-          raw[0][u] = (int16_t)(w[u] & 0xffffu);  // band plane 0 at the lower address
-          raw[1][u] = (int16_t)(w[u] >> 16);
+          raw[0][u] = (int32_t)__builtin_amdgcn_sbfe(w[u], 0, 16);  // band plane 0: lower address
+          // (the builtin returns unsigned: the cast keeps the sign-extended bits)
+          raw[1][u] = w[u] >> 16;
         }
       } else {
 #pragma unroll
@@ -238,19 +218,40 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
                            s * in.band_stride + (live ? p : 0) * in.band_pix_stride];
         }
       }
-      const int sh = 32 - lin_type_bits(LN.wrap_type);
+      // the sum modulo 2^32: a 24-bit multiply-add per band
+      int32_t acc[WB];
+#pragma unroll
+      for (int u = 0; u < WB; u++) {
+        acc[u] = (int32_t)(uint32_t)LN.c0;
+#pragma unroll
+        for (int s = 0; s < LT_LIN_MAX_BANDS; s++)
+          if (s < nb) acc[u] = __mul24((int)LN.coef[s], raw[s][u]) + acc[u];
+      }
+      const int wb = lin_type_bits(LN.wrap_type);
       const bool sgn = lin_type_signed(LN.wrap_type);
-      int64_t lo64, hi64;
+      int64_t lo64, hi64, wlo, whi;
       lin_out_range(LN.out_type, lo64, hi64);
+      lin_out_range(LN.wrap_type, wlo, whi);
+      // launch-uniform fast case ('B1 - B2': int16 nodes stored as int16 or binary64): a signed
+      // wrap (one bit-field extract, none for 32 bits) into a store type that holds every wrapped
+      // value, so the clamp is the identity, and an exact conversion
+      if (sgn && lo64 <= wlo && hi64 >= whi && LN.out_type != LT_T_F32) {
+        if (wb < 32) {
+#pragma unroll
+          for (int u = 0; u < WB; u++) val[u] = (double)(int32_t)__builtin_amdgcn_sbfe(acc[u], 0, wb);
+        } else {
+#pragma unroll
+          for (int u = 0; u < WB; u++) val[u] = (double)acc[u];
+        }
+        return;
+      }
+      const int sh = 32 - wb;
       const int32_t lo = lo64 < INT32_MIN ? INT32_MIN : (int32_t)lo64;
       const int32_t hi = hi64 > INT32_MAX ? INT32_MAX : (int32_t)hi64;
 #pragma unroll
       for (int u = 0; u < WB; u++) {
-        uint32_t acc = (uint32_t)LN.c0;
-#pragma unroll
-        for (int s = 0; s < LT_LIN_MAX_BANDS; s++)
-          if (s < nb) acc += (uint32_t)__mul24((int)LN.coef[s], (int)raw[s][u]);
-        const int32_t r = sgn ? (int32_t)(acc << sh) >> sh : (int32_t)((acc << sh) >> sh);
+        const uint32_t a = (uint32_t)acc[u];
+        const int32_t r = sgn ? (int32_t)(a << sh) >> sh : (int32_t)((a << sh) >> sh);
         if (LN.out_type == LT_T_F64) val[u] = (double)r;
         else if (LN.out_type == LT_T_F32) val[u] = (double)(float)r;
         else val[u] = (double)(r < lo ? lo : r > hi ? hi : r);

@@ -62,14 +62,19 @@ int64_t lt_lzw_decode(const uint8_t* in, int64_t n_in, uint8_t* out, int64_t cap
     len[c] = 1;
   }
   int nbits = 9, free_ent = kFirst, old = -1;
-  int64_t bitpos = 0, n_out = 0;
-  const int64_t total_bits = n_in * 8;
+  int64_t n_out = 0, byte_pos = 0;
+  // bit reader: whole bytes into a 64-bit buffer, codes taken from its top (MSB first); a code
+  // the remaining input cannot fill ends the strip
+  uint64_t bitbuf = 0;
+  int nbuf = 0;
   auto get = [&](int nb) -> int {
-    if (bitpos + nb > total_bits) return -1;
-    int v = 0;
-    for (int k = 0; k < nb; k++, bitpos++)
-      v = (v << 1) | ((in[bitpos >> 3] >> (7 - (bitpos & 7))) & 1);
-    return v;
+    while (nbuf < nb) {
+      if (byte_pos >= n_in) return -1;
+      bitbuf = (bitbuf << 8) | in[byte_pos++];
+      nbuf += 8;
+    }
+    nbuf -= nb;
+    return (int)((bitbuf >> nbuf) & ((1u << nb) - 1u));
   };
   auto emit = [&](int code) -> bool {
     const int L = len[code];

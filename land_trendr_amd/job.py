@@ -168,6 +168,11 @@ class LocalJob:
         for t in m.mine:
             bands = torch.from_numpy(np.ascontiguousarray(
                 st['bands'][:, slots, t.p0:t.p1])).to(dev)
+            if cuda and fn.lin is not None and len(slots) == 2 and bands.dtype == torch.int16:
+                # the fused load stage reads a pixel's two int16 bands as one 32-bit word
+                inter = torch.empty((K, t.n, 2), dtype=bands.dtype, device=dev).permute(0, 2, 1)
+                inter.copy_(bands)
+                bands = inter
             valid = torch.from_numpy(np.ascontiguousarray(st['valid'][:, t.p0:t.p1])).to(dev)
             vals = torch.empty((K, t.n), dtype=bands.dtype, device=dev)
             items.append(TileInput(t, self.scene, vals, valid, bands))
