@@ -31,7 +31,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from land_trendr_amd.distributed import Mosaic, TrendlineStream  # noqa: E402
-from land_trendr_amd.engine import get_engine  # noqa: E402
+from land_trendr_amd.engine import get_engine, valid_bytes  # noqa: E402
 from land_trendr_amd.index_eqn import IndexProgram  # noqa: E402
 from land_trendr_amd.runner import MosaicRunner  # noqa: E402
 from land_trendr_amd.scene import build_scene, parse_date  # noqa: E402
@@ -177,7 +177,8 @@ def parity_sample(runner, params, n_sample, threads, seed=12345):
             runner.materialise_index(k)
         cols = torch.from_numpy(flat[tile_of == k] - starts[k]).to(it.values.device)
         vals = it.values[:, cols].double().cpu().numpy()
-        valid = None if it.valid is None else it.valid[:, cols].cpu().numpy()
+        valid = None if it.valid is None else valid_bytes(it.valid[:, cols],
+                                                          it.scene.n_obs).cpu().numpy()
         exp = oracle.analyze_tile(it.scene, params, vals, valid, n_threads=threads)
         m = exp['matched'].astype(bool)
         for f, plane in runner.outs[k].items():
@@ -333,7 +334,8 @@ def main():
     items = mosaic_inputs(mosaic, cfg['years'], cfg['k'][0], cfg['k'][1], cfg['mask'],
                           cfg['seed'], dev, TARGET,
                           band_layout=os.environ.get('LT_BAND_LAYOUT',
-                                                     'pixel' if fused else 'planar'))
+                                                     'pixel' if fused else 'planar'),
+                          mask_format=os.environ.get('LT_MASK_FORMAT', 'bits'))
     params, rules = compile_params(cfg['line_cost'], cfg['rules'], cfg['mode'])
     eng = get_engine(local)
     index_fn = eng.compile_index(IndexProgram('B1 - B2', band_dtype='int16'))

@@ -33,6 +33,7 @@ extern "C" {
 #define LT_MAX_OBS 1024   /* observations per scene (K*T) */
 #define LT_MAX_RULES 16
 #define LT_NODATA (-99)   /* settings.py:16 */
+#define LT_MAX_TILE_PIX (1LL << 28) /* pixels per analyzed tile (lt_tile_in.n_pix)           */
 
 /* Per-pixel status bits (lt_tile_out.status). Non-zero = the reference raises for this pixel. */
 enum {
@@ -131,6 +132,10 @@ typedef struct {
   int64_t band_stride;        /* elements between bands of one obs at one pixel             */
   int64_t band_pix_stride;    /* elements between consecutive pixels of one band            */
   lt_index_lin lin;
+  /* the cloud mask as bit planes: bit (o % 32) of obs_valid_bits[(o / 32)*stride + p] is 1 when
+   * obs o is valid at pixel p (utils.py:353); used instead of obs_valid when set. The winner pick
+   * then reads ceil(K/32) words per pixel instead of one byte per observation */
+  const uint32_t* obs_valid_bits;
 } lt_tile_in;
 
 /* ---- load stage: settings.json index_eqn (utils.py:447-484 rast_algebra) -------------------- */

@@ -71,7 +71,7 @@ class LtTileIn(ctypes.Structure):
                 ('index_type', ctypes.c_int32), ('_pad', ctypes.c_int32),
                 ('obs_bands', ctypes.c_void_p), ('band_obs_stride', ctypes.c_int64),
                 ('band_stride', ctypes.c_int64), ('band_pix_stride', ctypes.c_int64),
-                ('lin', LtIndexLin)]
+                ('lin', LtIndexLin), ('obs_valid_bits', ctypes.c_void_p)]
 
 
 class LtIndexOp(ctypes.Structure):

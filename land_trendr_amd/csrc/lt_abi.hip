@@ -296,6 +296,7 @@ static int check_tile(lt_ctx* c, const lt_tile_in* in, const lt_tile_out* out) {
   if (!in || !out) return fail(c, LT_ERR_ARG, "null argument%s");
   if (in->n_pix < 0 || in->stride < in->n_pix || out->stride < in->n_pix)
     return fail(c, LT_ERR_ARG, "bad n_pix/stride%s");
+  if (in->n_pix > LT_MAX_TILE_PIX) return fail(c, LT_ERR_LIMIT, "tile above LT_MAX_TILE_PIX%s");
   if (in->n_pix == 0) return LT_OK;  // nothing is read or written
   if (in->obs_bands) {  // the fused load stage: a linear form lt_index_linearize accepts
     const lt_index_lin& L = in->lin;

@@ -149,6 +149,21 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
   // years in batches of 8: the winners first, then their 8 value loads issued together (one
   // load per year in sequence would leave each wave waiting out the HBM latency 30 times)
   constexpr int WB = LT_WB;
+  // the mask as bit planes (lt_tile_in.obs_valid_bits): up to 128 observations, the pixel's
+  // words are loaded once, together, and the winner scan tests bits; a byte mask costs a load
+  // per observation, each waited out before its year's comparison
+  const bool masked = in.obs_valid != nullptr || in.obs_valid_bits != nullptr;  // launch-uniform
+  const bool vbits = in.obs_valid_bits != nullptr && S.n_obs <= 128;
+  uint32_t vw0 = 0, vw1 = 0, vw2 = 0, vw3 = 0;
+  if (vbits) {
+    const uint32_t* vb = in.obs_valid_bits;
+    const int64_t pq = live ? p : 0;
+    const int nw = (S.n_obs + 31) >> 5;
+    vw0 = vb[pq];
+    if (nw > 1) vw1 = vb[is + pq];
+    if (nw > 2) vw2 = vb[2 * is + pq];
+    if (nw > 3) vw3 = vb[3 * is + pq];
+  }
   for (int yb = 0; yb < Y; yb += WB) {
     int best[WB];
 #pragma unroll
@@ -156,7 +171,7 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
       const int y = yb + u;
       best[u] = -1;
       if (y >= Y) continue;  // wave-uniform
-      if (in.obs_valid == nullptr) {  // launch-uniform: no mask, the scene's winner
+      if (!masked) {  // launch-uniform: no mask, the scene's winner
         best[u] = live ? S.winner_all[y] : -1;
         continue;
       }
@@ -164,7 +179,13 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
       const int k1 = S.slot_begin[y + 1];
       for (int k = S.slot_begin[y]; k < k1; k++) {
         const int o = S.order[k];
-        const bool ok = live && in.obs_valid[(int64_t)o * is + p] != 0;
+        bool ok;
+        if (vbits) {  // o is wave-uniform: a scalar choice of the word
+          const uint32_t wd = o < 32 ? vw0 : o < 64 ? vw1 : o < 96 ? vw2 : vw3;
+          ok = live && ((wd >> (o & 31)) & 1u);
+        } else {
+          ok = live && obs_is_valid(in, o, p);
+        }
         if (ok && S.dist[k] < bd) {
           bd = S.dist[k];
           best[u] = o;
@@ -172,15 +193,26 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
       }
     }
     double val[WB];
-    // unconditional loads (obs 0 / pixel 0 stand in), one typed batch per launch-uniform type:
-    // all WB loads in flight at once
-    auto batch = [&](auto tag) {
+    // Loads of the batch: unconditional (obs 0 / pixel 0 stand in), all WB in flight at once, one
+    // typed batch per launch-uniform type. Without a cloud mask every lane's winner of a year is
+    // the scene's (uniform: UNI), so a load is the row's base in SGPRs plus the lane's 32-bit
+    // offset — no per-lane 64-bit address arithmetic; with a mask each lane has its own row.
+    const uint32_t pp = live ? (uint32_t)p : 0u;  // pixel offset within a row
+    __builtin_assume(pp < (1u << 28));             // tiles hold <= LT_MAX_TILE_PIX pixels
+    auto row_of = [&](int u, auto uni) -> int64_t {
+      if constexpr (decltype(uni)::value) {
+        const int w = yb + u < Y ? S.winner_all[yb + u] : 0;
+        return w > 0 ? w : 0;
+      } else {
+        return best[u] >= 0 ? best[u] : 0;
+      }
+    };
+    auto batch = [&](auto tag, auto uni) {
       using T = decltype(tag);
       const T* base = in.obs_index ? (const T*)in.obs_index : (const T*)in.obs_val;
       T raw[WB];
 #pragma unroll
-      for (int u = 0; u < WB; u++)
-        raw[u] = base[(int64_t)(best[u] >= 0 ? best[u] : 0) * is + (live ? p : 0)];
+      for (int u = 0; u < WB; u++) raw[u] = (base + row_of(u, uni) * is)[pp];
 #pragma unroll
       for (int u = 0; u < WB; u++) val[u] = (double)raw[u];
     };
@@ -190,42 +222,39 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
     // clamp, one conversion (the sum is needed only modulo 2^bits(node type) <= 2^32). Other forms
     // take obs_value's general path (lt_pixel.h lin_value), one value at a time: one instance of
     // the batch keeps the kernel's code and register allocation as they are without it
-    auto fused16 = [&]() {
-      const int16_t* bb = (const int16_t*)in.obs_bands;
+    auto fused16 = [&](auto uni) {
       const lt_index_lin& LN = in.lin;
       const int nb = LN.n_bands;
-      int32_t raw[LT_LIN_MAX_BANDS][WB];  // sign-extended band values
+      int32_t acc[WB];  // the sum modulo 2^32: a 24-bit multiply-add per band
       if (nb == 2 && in.band_stride == 1) {  // a pixel-interleaved pair: one 32-bit load
         const int32_t* bw = (const int32_t*)in.obs_bands;
         const int64_t os2 = in.band_obs_stride >> 1;
         int32_t w[WB];
 #pragma unroll
-        for (int u = 0; u < WB; u++)
-          w[u] = bw[(int64_t)(best[u] >= 0 ? best[u] : 0) * os2 + (live ? p : 0)];
+        for (int u = 0; u < WB; u++) w[u] = (bw + row_of(u, uni) * os2)[pp];
+        const int c0 = (int)(uint32_t)LN.c0, k0 = (int)LN.coef[0], k1 = (int)LN.coef[1];
 #pragma unroll
         for (int u = 0; u < WB; u++) {
-          raw[0][u] = (int32_t)__builtin_amdgcn_sbfe(w[u], 0, 16);  // band plane 0: lower address
-          // (the builtin returns unsigned: the cast keeps the sign-extended bits)
-          raw[1][u] = w[u] >> 16;
+          // band plane 0 at the lower address (the builtin returns unsigned: the cast keeps the
+          // sign-extended bits)
+          const int b0 = (int32_t)__builtin_amdgcn_sbfe(w[u], 0, 16), b1 = w[u] >> 16;
+          acc[u] = __mul24(k1, b1) + (__mul24(k0, b0) + c0);
         }
       } else {
+        const int16_t* bb = (const int16_t*)in.obs_bands;
+#pragma unroll
+        for (int u = 0; u < WB; u++) acc[u] = (int32_t)(uint32_t)LN.c0;
 #pragma unroll
         for (int s = 0; s < LT_LIN_MAX_BANDS; s++) {
           if (s >= nb) break;  // launch-uniform
+          int16_t raw[WB];
 #pragma unroll
           for (int u = 0; u < WB; u++)
-            raw[s][u] = bb[(int64_t)(best[u] >= 0 ? best[u] : 0) * in.band_obs_stride +
-                           s * in.band_stride + (live ? p : 0) * in.band_pix_stride];
+            raw[u] = bb[row_of(u, uni) * in.band_obs_stride + s * in.band_stride +
+                        (int64_t)pp * in.band_pix_stride];
+#pragma unroll
+          for (int u = 0; u < WB; u++) acc[u] = __mul24((int)LN.coef[s], (int)raw[u]) + acc[u];
         }
-      }
-      // the sum modulo 2^32: a 24-bit multiply-add per band
-      int32_t acc[WB];
-#pragma unroll
-      for (int u = 0; u < WB; u++) {
-        acc[u] = (int32_t)(uint32_t)LN.c0;
-#pragma unroll
-        for (int s = 0; s < LT_LIN_MAX_BANDS; s++)
-          if (s < nb) acc[u] = __mul24((int)LN.coef[s], raw[s][u]) + acc[u];
       }
       const int wb = lin_type_bits(LN.wrap_type);
       const bool sgn = lin_type_signed(LN.wrap_type);
@@ -257,6 +286,9 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
         else val[u] = (double)(r < lo ? lo : r > hi ? hi : r);
       }
     };
+    using Uni = std::true_type;
+    using Lane = std::false_type;
+    const bool uni = !masked;  // launch-uniform
     if (in.obs_bands) {
       const lt_index_lin& LN = in.lin;
       const int wb = lin_type_bits(LN.wrap_type);
@@ -266,19 +298,28 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
       for (int s = 0; s < LT_LIN_MAX_BANDS; s++)
         if (s < LN.n_bands) narrow = narrow && LN.coef[s] >= -(1 << 23) && LN.coef[s] < (1 << 23);
       if (narrow) {
-        fused16();
+        if (uni) fused16(Uni{});
+        else fused16(Lane{});
       } else {
 #pragma unroll
         for (int u = 0; u < WB; u++)
           val[u] = obs_value(in, (int64_t)(best[u] >= 0 ? best[u] : 0), live ? p : 0);
       }
-    } else if (in.obs_index == nullptr) batch(double{});
-    else if (in.index_type == LT_T_I16) batch(int16_t{});
-    else if (in.index_type == LT_T_F32) batch(float{});
-    else if (in.index_type == LT_T_U16) batch(uint16_t{});
-    else if (in.index_type == LT_T_I32) batch(int32_t{});
-    else if (in.index_type == LT_T_U8) batch(uint8_t{});
-    else {
+    } else if (in.obs_index == nullptr) {
+      if (uni) batch(double{}, Uni{});
+      else batch(double{}, Lane{});
+    } else if (in.index_type == LT_T_I16) {
+      if (uni) batch(int16_t{}, Uni{});
+      else batch(int16_t{}, Lane{});
+    } else if (in.index_type == LT_T_F32) {
+      batch(float{}, Lane{});
+    } else if (in.index_type == LT_T_U16) {
+      batch(uint16_t{}, Lane{});
+    } else if (in.index_type == LT_T_I32) {
+      batch(int32_t{}, Lane{});
+    } else if (in.index_type == LT_T_U8) {
+      batch(uint8_t{}, Lane{});
+    } else {
 #pragma unroll
       for (int u = 0; u < WB; u++)
         val[u] = obs_value(in, (int64_t)(best[u] >= 0 ? best[u] : 0), live ? p : 0);

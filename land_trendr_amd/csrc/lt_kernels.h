@@ -56,17 +56,6 @@ template <int MAXY, int RMAX, class VT, int WAVES, class Probe>
 __global__ __launch_bounds__(64, WAVES) void analyze_fast_kernel(const KernelArgs A) {
   (void)A;  // read through args()
   __shared__ WaveLds<MAXY, VT, false> L;
-#if defined(LT_STAGGER_NS) && LT_STAGGER_NS > 0
-  // first resident generation: wave b waits one of 64 steps of LT_STAGGER_NS (spread over the
-  // waves of each CU), so the phases of resident waves do not stay aligned
-  if (blockIdx.x < 4096) {
-    const unsigned b = blockIdx.x;
-    const uint64_t steps = ((b >> 8) & 15) * 4 + ((b >> 3) & 3);
-    const uint64_t t0 = wall_clock64();
-    const uint64_t wait = steps * (uint64_t)(LT_STAGGER_NS / 640);  // 100 MHz ticks
-    while (wall_clock64() - t0 < wait) __builtin_amdgcn_s_sleep(16);
-  }
-#endif
   const KernelArgs& K = args();
   const int lane = threadIdx.x;
   const int64_t p = (int64_t)blockIdx.x * 64 + lane;

@@ -292,6 +292,13 @@ __host__ __device__ inline double lin_value(const lt_tile_in& in, int64_t o, int
   return lin_store(L, acc);
 }
 
+// Whether observation o is valid (not cloud-masked, utils.py:353) at pixel p: the byte mask, the
+// mask bit planes, or no mask.
+__host__ __device__ inline bool obs_is_valid(const lt_tile_in& in, int64_t o, int64_t p) {
+  if (in.obs_valid_bits) return (in.obs_valid_bits[(o >> 5) * in.stride + p] >> (o & 31)) & 1u;
+  return in.obs_valid == nullptr || in.obs_valid[o * in.stride + p] != 0;
+}
+
 // Value of observation o at pixel p of a tile: the f64 values, the index raster in its stored
 // type (float(val), utils.py:357), or the fused load stage's value from the band planes.
 // index_type is uniform over a launch: a scalar branch on the GPU.
@@ -588,7 +595,7 @@ __host__ __device__ bool analyze_pixel(const DevScene& S, const lt_params& P, co
     const int k1 = S.slot_begin[y + 1];
     for (int k = S.slot_begin[y]; k < k1; k++) {
       const int o = S.order[k];
-      const bool ok = in.obs_valid == nullptr || in.obs_valid[(int64_t)o * is + p] != 0;
+      const bool ok = obs_is_valid(in, o, p);
       if (ok && S.dist[k] < bd) {
         bd = S.dist[k];
         best = o;

@@ -139,7 +139,15 @@ class Engine:
             K, P = values.shape
         if K != scene.n_obs:
             raise LtError('values has %d obs rows, scene has %d' % (K, scene.n_obs))
-        if valid is not None:
+        if valid is not None and valid.dtype == torch.int32:  # mask bit planes
+            W = (K + 31) // 32
+            if (tuple(valid.shape) != (W, P) or valid.stride(1) != 1 or
+                    valid.device != self.device):
+                raise LtError('valid bit planes must be an int32 [%d, P] tensor with unit pixel '
+                              'stride' % W)
+            if lin is None and W > 1 and valid.stride(0) != values.stride(0):
+                raise LtError('valid bit planes must share the row stride of values')
+        elif valid is not None:
             if lin is not None:
                 if (valid.dtype != torch.uint8 or tuple(valid.shape) != (K, P) or
                         valid.stride(1) != 1 or valid.device != self.device):
@@ -166,7 +174,7 @@ class Engine:
         tin = _abi.LtTileIn()
         tin.n_pix = P
         if lin is not None:
-            tin.stride = valid.stride(0) if valid is not None else P
+            tin.stride = valid.stride(0) if valid is not None and valid.shape[0] > 1 else P
             tin.obs_bands = values.data_ptr()
             tin.band_obs_stride = values.stride(0)
             tin.band_stride = values.stride(1)
@@ -179,7 +187,11 @@ class Engine:
             tin.stride = values.stride(0)
             tin.obs_index = values.data_ptr()
             tin.index_type = _LT_T[values.dtype]
-        tin.obs_valid = ctypes.cast(valid.data_ptr(), _abi.c_u8p) if valid is not None else None
+        if valid is not None and valid.dtype == torch.int32:
+            tin.obs_valid_bits = valid.data_ptr()
+        else:
+            tin.obs_valid = (ctypes.cast(valid.data_ptr(), _abi.c_u8p) if valid is not None
+                             else None)
         tout = _abi.LtTileOut()
         tout.stride = ostride if ostride is not None else P
         for f, t in out.items():
@@ -250,6 +262,24 @@ class Engine:
         n = ctypes.c_int64()
         self._check(self.lib.lt_ctx_last_deferred(self.ctx, ctypes.byref(n)), 'last_deferred')
         return n.value
+
+
+def pack_valid_bits(valid):
+    """A [K, P] cloud mask (nonzero = valid, utils.py:353) as the bit planes the analyze kernel
+    reads (lt_tile_in.obs_valid_bits): int32 [ceil(K/32), P], bit k % 32 of plane k // 32."""
+    K, P = valid.shape
+    acc = torch.zeros(((K + 31) // 32, P), dtype=torch.int64, device=valid.device)
+    for k in range(K):
+        acc[k // 32] |= (valid[k] != 0).to(torch.int64) << (k % 32)
+    return acc.to(torch.int32)
+
+
+def valid_bytes(valid, n_obs):
+    """The [K, P] uint8 mask of either form (bytes, or pack_valid_bits planes)."""
+    if valid is None or valid.dtype == torch.uint8:
+        return valid
+    return torch.stack([((valid[k // 32] >> (k % 32)) & 1).to(torch.uint8)
+                        for k in range(n_obs)])
 
 
 class IndexFn:

@@ -137,7 +137,7 @@ class LocalJob:
         job's trendline. Returns the writer's label planes (device), None on the other ranks."""
         import torch
         from .distributed import Mosaic, TrendlineStream
-        from .engine import LABELS, TRENDLINE, get_engine
+        from .engine import LABELS, TRENDLINE, get_engine, pack_valid_bits
         from .index_eqn import IndexProgram
         from .runner import MosaicRunner, TileInput
         from .scene import build_scene, parse_date
@@ -174,6 +174,8 @@ class LocalJob:
                 inter.copy_(bands)
                 bands = inter
             valid = torch.from_numpy(np.ascontiguousarray(st['valid'][:, t.p0:t.p1])).to(dev)
+            if cuda:  # the winner pick reads the mask as bit planes (one word per 32 obs)
+                valid = pack_valid_bits(valid)
             vals = torch.empty((K, t.n), dtype=bands.dtype, device=dev)
             items.append(TileInput(t, self.scene, vals, valid, bands))
         host = self.host_trendline = self._trendline_planes(tl_fields, Y, P, dist, world, rank)

@@ -97,12 +97,13 @@ def make_scene(n_pix, n_years=30, k_min=1, k_max=1, mask_prob=0.0, first_year=19
 
 
 def mosaic_inputs(mosaic, n_years, k_min=1, k_max=1, mask_prob=0.0, seed0=1000, device='cpu',
-                  target_date='2014-07-01', band_layout='pixel'):
+                  target_date='2014-07-01', band_layout='pixel', mask_format='bits'):
     """runner.TileInput for every tile this rank owns in `mosaic`: scene s is the seeded scene
     make_scene(seed=seed0 + s) as int16 bands (B1, B2) + cloud mask, so a tile's content does not
     depend on the number of ranks. A rank owning a whole scene keeps it in place (tiles are views
     sharing one index raster); otherwise its tiles are copied out and the scene freed. Bands are
-    pixel-interleaved by default (make_scene band_layout)."""
+    pixel-interleaved by default (make_scene band_layout); cloud masks are bit planes by default
+    (engine.pack_valid_bits; mask_format='bytes' keeps the [K, P] uint8 mask)."""
     from .runner import TileInput
     from .scene import build_scene, parse_date
     items = []
@@ -112,6 +113,9 @@ def mosaic_inputs(mosaic, n_years, k_min=1, k_max=1, mask_prob=0.0, seed0=1000, 
                         mask_prob=mask_prob, seed=seed0 + s, device=dev, with_bands=True,
                         band_layout=band_layout)
         sc.values = None  # only the bands travel (the load stage computes the index raster)
+        if sc.valid is not None and mask_format == 'bits':
+            from .engine import pack_valid_bits
+            sc.valid = pack_valid_bits(sc.valid)
         meta = build_scene(sc.dates, parse_date(target_date))
         mine = [t for t in mosaic.mine if t.scene == s]
         whole = len(mine) == sum(1 for t in mosaic.tiles if t.scene == s)

@@ -13,10 +13,13 @@
 #ifndef LT_PROBE_RMAX
 #define LT_PROBE_RMAX 1
 #endif
+#ifndef LT_PROBE_WAVES
+#define LT_PROBE_WAVES 4
+#endif
 
 namespace lt {
 hipError_t launch_analyze(const TileLaunch& l) {
-  return launch_analyze_instance<LT_PROBE_MAXY, LT_PROBE_RMAX, 4, LT_PROBE>(l);
+  return launch_analyze_instance<LT_PROBE_MAXY, LT_PROBE_RMAX, LT_PROBE_WAVES, LT_PROBE>(l);
 }
 hipError_t launch_resolve(const TileLaunch& l) { return launch_resolve_instance<LT_PROBE_MAXY, LT_PROBE_RMAX>(l); }
 }  // namespace lt

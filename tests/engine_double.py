@@ -22,9 +22,11 @@ class OracleEngine:
 
     def analyze_tiles(self, scene, params, tiles, fields, outs=None, ready=None):
         from oracle import oracle
+        from land_trendr_amd.engine import valid_bytes
         for (vals, valid), o in zip(tiles, outs):
             want = oracle.analyze_tile(scene, params, vals.numpy().astype(np.float64),
-                                       None if valid is None else valid.numpy())
+                                       None if valid is None else
+                                       valid_bytes(valid, scene.n_obs).numpy())
             for f in fields:
                 o[f].copy_(torch.from_numpy(want[f][..., :o[f].shape[-1]]))
         return outs

@@ -28,7 +28,7 @@ sys.path.insert(0, ROOT)
 
 import bench  # noqa: E402
 from land_trendr_amd.distributed import Mosaic  # noqa: E402
-from land_trendr_amd.engine import get_engine  # noqa: E402
+from land_trendr_amd.engine import get_engine, valid_bytes  # noqa: E402
 from land_trendr_amd.index_eqn import IndexProgram  # noqa: E402
 from land_trendr_amd.runner import MosaicRunner  # noqa: E402
 from land_trendr_amd.settings import compile_params  # noqa: E402
@@ -83,7 +83,8 @@ def main():
                 continue
             sl = slice(lo - it.tile.p0, hi - it.tile.p0)
             vals = it.values[:, sl].double().cpu().numpy()
-            valid = it.valid[:, sl].cpu().numpy() if it.valid is not None else None
+            valid = (valid_bytes(it.valid[:, sl], meta.n_obs).cpu().numpy()
+                     if it.valid is not None else None)
             want = oracle.analyze_tile(meta, params, vals, valid, n_threads=threads)
             for f in fields:
                 x = want[f]

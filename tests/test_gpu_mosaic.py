@@ -14,7 +14,7 @@ import torch
 
 import bench
 from land_trendr_amd.distributed import Mosaic, TrendlineStream
-from land_trendr_amd.engine import get_engine
+from land_trendr_amd.engine import get_engine, valid_bytes
 from land_trendr_amd.index_eqn import IndexProgram
 from land_trendr_amd.runner import MosaicRunner
 from land_trendr_amd.settings import compile_params
@@ -88,7 +88,8 @@ def test_bench_path_full_size_sampled_vs_oracle(cfg):
             idx = torch.from_numpy(np.sort(rng.choice(it.tile.n, share, replace=False))).to(
                 it.values.device)
             vals = it.values[:, idx].double().cpu().numpy()
-            valid = it.valid[:, idx].cpu().numpy() if it.valid is not None else None
+            valid = (valid_bytes(it.valid[:, idx], it.scene.n_obs).cpu().numpy()
+                     if it.valid is not None else None)
             want = oracle.analyze_tile(it.scene, params, vals, valid, n_threads=_threads())
             for f in fields:
                 a = want[f]
