@@ -89,14 +89,16 @@ def pmc_summary(config):
     """The committed rocprofv3 --pmc summary of this build for `config` (profiles/
     summarize_pmc.py: per-launch counters of one 16.8 Mpx launch; c4 runs c2's kernel instance)."""
     name = {'c4': 'c2'}.get(config, config)
-    path = os.path.join(ROOT, 'profiles', 'r02_pmc_%s.json' % name)
-    try:
-        with open(path) as f:
-            d = json.load(f)
-        d['_path'] = os.path.relpath(path, ROOT)
-        return d
-    except (OSError, ValueError):
-        return None
+    for rnd in ('r03', 'r02'):  # the newest summary committed for this config
+        path = os.path.join(ROOT, 'profiles', '%s_pmc_%s.json' % (rnd, name))
+        try:
+            with open(path) as f:
+                d = json.load(f)
+            d['_path'] = os.path.relpath(path, ROOT)
+            return d
+        except (OSError, ValueError):
+            continue
+    return None
 
 
 def per_px(pmc, kernel, counter):

@@ -163,14 +163,18 @@ void launch_resolve1(const TileLaunch& l, int64_t* list, unsigned long long* cou
 }
 
 // both deferred lists: the first in the tile's series type, the second (values binary32 cannot
-// hold) in binary64
+// hold) in binary64. An int16 series is exact in binary32, so its second list is always empty and
+// is not launched: the launch's resident-size grid of waves that find nothing to do still took
+// CU slots beside the next tile's analyze waves (3.9 ms of trace time per tile on c2,
+// profiles/r03_c2_kernel_stats_head.csv)
 template <int MAXY, int RMAX>
 hipError_t launch_resolve_instance(const TileLaunch& l) {
   const SeriesKind k = series_kind(l);
   if (k == kSeriesI16) launch_resolve1<MAXY, RMAX, int16_t>(l, l.defer, l.counters);
   else if (k == kSeriesF64) launch_resolve1<MAXY, RMAX, double>(l, l.defer, l.counters);
   else launch_resolve1<MAXY, RMAX, float>(l, l.defer, l.counters);
-  launch_resolve1<MAXY, RMAX, double>(l, l.defer + l.in->n_pix, l.counters + 2);
+  if (k != kSeriesI16)
+    launch_resolve1<MAXY, RMAX, double>(l, l.defer + l.in->n_pix, l.counters + 2);
   return hipGetLastError();
 }
 

@@ -905,18 +905,14 @@ __host__ __device__ inline int lstsq_xint(int m, GX X, GY Y, bool need_solution,
 
 // ------------------------------------------------------------------------------------------------
 // Table of lsq_factor results for the x-sets segments usually have (year offsets < 64): m = 2
-// with a gap <= 16, m = 3 with gaps <= 8, m = 4 with gaps <= 4, m >= 5 consecutive years, and
-// m = 5..8 with gaps of 1 or 2 years (a spike or a cloud-masked year inside a segment: at
-// line_cost 1 the factorisations on the fly for those cost 4 % of the c5 analyze launch,
-// profiles/r03_pmc3). Built on the device once per context (lt_abi.hip); lookups that miss factor
-// on the fly.
+// with a gap <= 16, m = 3 with gaps <= 8, m = 4 with gaps <= 4, and m >= 5 consecutive years.
+// Built on the device once per context (lt_abi.hip); lookups that miss factor on the fly. (Slots
+// for 5-8 point x-sets with gaps of 1-2 years were tried: the key's loop, inlined into the
+// year-major output loop, spilled 29 VGPRs of the c5 instance, 986 vs 1190 Mpx/s,
+// profiles/r03_ab6; taken only in the miss branch it still spilled 14.)
 // ------------------------------------------------------------------------------------------------
 constexpr int kXtM2 = 0, kXtM3 = 64 * 16, kXtM4 = kXtM3 + 64 * 64, kXtCons = kXtM4 + 64 * 64,
-              kXtG5 = kXtCons + 64 * 64,  // m = 5..8, gaps in {1, 2}: 64 x0 * 2^(m-1) patterns
-              kXtSize = kXtG5 + 64 * (16 + 32 + 64 + 128);
-__host__ __device__ constexpr int xt_gap_base(int m) {  // first slot of the m-point gap patterns
-  return kXtG5 + 64 * ((1 << (m - 1)) - 16);
-}
+              kXtSize = kXtCons + 64 * 64;
 
 // table slot of the x-set X(0) < ... < X(m-1) (all < 64), or -1
 template <class GX>
@@ -939,16 +935,6 @@ __host__ __device__ inline int xset_key(int m, GX X) {
                : -1;
   }
   if (m >= 5 && m <= 64 && X(m - 1) - x0 == m - 1) return kXtCons + x0 * 64 + (m - 1);
-  if (m >= 5 && m <= 8) {  // gaps of 1 or 2 (bit k-1: gap k is 2), not all 1 (consecutive above)
-    int pat = 0, xp = x0;
-    for (int k = 1; k < m; k++) {
-      const int xk = X(k), d = xk - xp;
-      if (d < 1 || d > 2) return -1;
-      pat |= (d - 1) << (k - 1);
-      xp = xk;
-    }
-    return xp <= 63 ? xt_gap_base(m) + x0 * (1 << (m - 1)) + pat : -1;
-  }
   return -1;
 }
 
@@ -972,20 +958,11 @@ __host__ __device__ inline bool xset_of_key(int idx, int& m, int* xs) {
     d[0] = (r / 16) % 4 + 1;
     d[1] = (r / 4) % 4 + 1;
     d[2] = r % 4 + 1;
-  } else if (idx < kXtG5) {
+  } else if (idx < kXtSize) {
     const int r = idx - kXtCons;
     m = r % 64 + 1;
     xs[0] = r / 64;
     if (m < 5) return false;
-  } else if (idx < kXtSize) {
-    m = 5;
-    while (m < 8 && idx >= xt_gap_base(m + 1)) m++;
-    const int r = idx - xt_gap_base(m), np = 1 << (m - 1);
-    const int pat = r % np;
-    xs[0] = r / np;
-    if (pat == 0) return false;  // consecutive: kXtCons
-    for (int k = 1; k < m; k++) xs[k] = xs[k - 1] + 1 + ((pat >> (k - 1)) & 1);
-    return xs[m - 1] <= 63;
   } else {
     return false;
   }
