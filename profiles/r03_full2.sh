@@ -1,0 +1,14 @@
+#!/bin/bash
+# Whole-scene parity at the round-3 build: every pixel of bench's c5 scene, all nine trendline
+# planes + labels, in two halves. Usage: bash profiles/r03_full2.sh <outdir under gpurun_out>
+set -e
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/$1
+mkdir -p $O
+cd $R
+timeout -k 10 540 python -u tests/full_scene_check.py --config c5 --first 0 --last 24500000 \
+  --out $O/full_c5_first_half.json > $O/full_c5a.log 2>&1
+tail -2 $O/full_c5a.log
+timeout -k 10 540 python -u tests/full_scene_check.py --config c5 --first 24500000 --last 49000000 \
+  --out $O/full_c5_second_half.json > $O/full_c5b.log 2>&1
+tail -2 $O/full_c5b.log
