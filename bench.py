@@ -217,10 +217,13 @@ class _PinnedBands:
     device slab k % 2 on a copy stream, once the load kernel of tile k - 2 has read that slab."""
 
     def __init__(self, items, dev):
-        # host copies and device slabs in the bands' own layout (planar or pixel-interleaved)
+        # host copies in the bands' own layout (planar or pixel-interleaved), compact; each device
+        # slab is flat and a tile's view of it has the host copy's exact strides, so every H2D is
+        # one contiguous copy (a shorter last tile sliced out of a full-size view had strides of
+        # the full tile and was not)
         self.host = [_pinned_like(it.bands) for it in items]
         big = max(self.host, key=lambda b: b.numel())
-        self.slab = [torch.empty_like(big, device=dev) for _ in range(2)]
+        self.slab = [torch.empty(big.numel(), dtype=big.dtype, device=dev) for _ in range(2)]
         self.free = [None, None]
         self.stream = torch.cuda.Stream(dev)
         self.bytes = 0
@@ -231,7 +234,7 @@ class _PinnedBands:
         with torch.cuda.stream(self.stream):
             if self.free[s] is not None:
                 self.stream.wait_event(self.free[s])
-            dst = self.slab[s][:, :, :h.shape[2]]
+            dst = self.slab[s][:h.numel()].as_strided(h.size(), h.stride())
             dst.copy_(h, non_blocking=True)
             ev = torch.cuda.Event()
             ev.record()

@@ -165,7 +165,10 @@ typedef struct {
   lt_index_op ops[LT_MAX_PROG];
 } lt_index_prog;
 /* Device buffers of one lt_index_apply: band s of obs o, pixel p at
- * bands[o*obs_stride + s*band_stride + p]; index of obs o, pixel p at out[o*out_stride + p]. */
+ * bands[o*obs_stride + s*band_stride + p*band_pix_stride]; index of obs o, pixel p at
+ * out[o*out_stride + p]. Planar bands: band_pix_stride 1 (or 0), band_stride >= n_pix.
+ * Pixel-interleaved bands (the layout lt_tile_in.obs_bands reads fastest): band_stride 1,
+ * band_pix_stride = the program's n_bands. */
 typedef struct {
   int64_t n_pix;
   int64_t n_obs;
@@ -174,6 +177,7 @@ typedef struct {
   int64_t out_stride;
   const void* bands;
   void* out;
+  int64_t band_pix_stride;
 } lt_index_io;
 typedef struct lt_index lt_index;
 

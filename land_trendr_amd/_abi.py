@@ -116,7 +116,7 @@ class LtIndexIO(ctypes.Structure):
     _fields_ = [('n_pix', ctypes.c_int64), ('n_obs', ctypes.c_int64),
                 ('obs_stride', ctypes.c_int64), ('band_stride', ctypes.c_int64),
                 ('out_stride', ctypes.c_int64), ('bands', ctypes.c_void_p),
-                ('out', ctypes.c_void_p)]
+                ('out', ctypes.c_void_p), ('band_pix_stride', ctypes.c_int64)]
 
 
 class LtTileOut(ctypes.Structure):

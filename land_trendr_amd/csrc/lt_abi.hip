@@ -659,7 +659,8 @@ int lt_index_compile(lt_ctx* c, const lt_index_prog* prog, lt_index** out) {
   f->out_type = prog->out_type;
   if (hipModuleLoadData(&f->mod, code.data()) != hipSuccess ||
       hipModuleGetFunction(&f->fn, f->mod, "lt_index_kernel") != hipSuccess ||
-      hipModuleGetFunction(&f->fn4, f->mod, "lt_index_kernel4") != hipSuccess) {
+      hipModuleGetFunction(&f->fn4, f->mod, "lt_index_kernel4") != hipSuccess ||
+      hipModuleGetFunction(&f->fn4i, f->mod, "lt_index_kernel4i") != hipSuccess) {
     if (f->mod) (void)hipModuleUnload(f->mod);
     delete f;
     return fail(c, LT_ERR_JIT, "module load failed%s");
@@ -680,32 +681,44 @@ int lt_index_apply(lt_ctx* c, const lt_index* f, const lt_index_io* io, void* st
   if (io->n_pix < 0 || io->n_obs < 0 || io->n_obs > 65535) return fail(c, LT_ERR_ARG, "bad sizes%s");
   if (io->n_pix == 0 || io->n_obs == 0) return LT_OK;
   if (!io->bands || !io->out) return fail(c, LT_ERR_ARG, "null buffer%s");
-  if (io->out_stride < io->n_pix || io->band_stride < io->n_pix ||
-      io->obs_stride < (int64_t)f->n_bands * io->band_stride)
+  // planar (pixel stride 1 or 0) or pixel-interleaved (band stride 1, pixel stride n_bands)
+  const bool inter = io->band_pix_stride > 1;
+  if (inter ? (io->band_pix_stride != f->n_bands || io->band_stride != 1 ||
+               io->obs_stride < (int64_t)f->n_bands * io->n_pix)
+            : (io->band_pix_stride < 0 || io->band_stride < io->n_pix ||
+               io->obs_stride < (int64_t)f->n_bands * io->band_stride))
     return fail(c, LT_ERR_ARG, "bad strides%s");
+  if (io->out_stride < io->n_pix) return fail(c, LT_ERR_ARG, "bad strides%s");
   HIP_OR_FAIL(c, hipSetDevice(c->device));
   long long obs_stride = io->obs_stride, band_stride = io->band_stride,
-            out_stride = io->out_stride;
+            out_stride = io->out_stride, pix_stride = inter ? io->band_pix_stride : 1;
   const size_t bsz = lt_idx::type_size(f->band_type), osz = lt_idx::type_size(f->out_type);
   // 4-pixel vector kernel over the 4-aligned head when every plane start is 4-element aligned
   const bool vec_ok = ((uintptr_t)io->bands % (4 * bsz)) == 0 &&
                       ((uintptr_t)io->out % (4 * osz)) == 0 && obs_stride % 4 == 0 &&
-                      band_stride % 4 == 0 && out_stride % 4 == 0;
+                      (inter || band_stride % 4 == 0) && out_stride % 4 == 0;
   const long long head = vec_ok ? (io->n_pix & ~3LL) : 0;
   if (head > 0) {
     const void* bands = io->bands;
     void* outp = io->out;
     long long n_pix = head;
-    void* args[] = {(void*)&bands, &obs_stride, &band_stride, &n_pix, &outp, &out_stride};
     const unsigned gx = (unsigned)((head / 4 + 255) / 256);
-    HIP_OR_FAIL(c, hipModuleLaunchKernel(f->fn4, gx, (unsigned)io->n_obs, 1, 256, 1, 1, 0,
-                                         (hipStream_t)stream_, args, nullptr));
+    if (inter) {
+      void* args[] = {(void*)&bands, &obs_stride, &n_pix, &outp, &out_stride};
+      HIP_OR_FAIL(c, hipModuleLaunchKernel(f->fn4i, gx, (unsigned)io->n_obs, 1, 256, 1, 1, 0,
+                                           (hipStream_t)stream_, args, nullptr));
+    } else {
+      void* args[] = {(void*)&bands, &obs_stride, &band_stride, &n_pix, &outp, &out_stride};
+      HIP_OR_FAIL(c, hipModuleLaunchKernel(f->fn4, gx, (unsigned)io->n_obs, 1, 256, 1, 1, 0,
+                                           (hipStream_t)stream_, args, nullptr));
+    }
   }
   if (head < io->n_pix) {
-    const void* bands = (const char*)io->bands + head * bsz;
+    const void* bands = (const char*)io->bands + head * pix_stride * bsz;
     void* outp = (char*)io->out + head * osz;
     long long n_pix = io->n_pix - head;
-    void* args[] = {(void*)&bands, &obs_stride, &band_stride, &n_pix, &outp, &out_stride};
+    void* args[] = {(void*)&bands, &obs_stride, &band_stride, &n_pix, &outp, &out_stride,
+                    &pix_stride};
     const unsigned gx = (unsigned)((n_pix + 255) / 256);
     HIP_OR_FAIL(c, hipModuleLaunchKernel(f->fn, gx, (unsigned)io->n_obs, 1, 256, 1, 1, 0,
                                          (hipStream_t)stream_, args, nullptr));

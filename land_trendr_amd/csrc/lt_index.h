@@ -16,7 +16,7 @@
 
 struct lt_index {
   hipModule_t mod = nullptr;
-  hipFunction_t fn = nullptr, fn4 = nullptr;
+  hipFunction_t fn = nullptr, fn4 = nullptr, fn4i = nullptr;
   int32_t n_bands = 0, band_type = 0, out_type = 0;
 };
 
@@ -110,9 +110,10 @@ inline std::string fmt_double(double d) {
   return b;
 }
 
-// Generated source for prog, or "" with err set. Two kernels: lt_index_kernel (one pixel per
-// thread) and lt_index_kernel4 (four consecutive pixels per thread, vector loads and stores, for
-// 4-aligned planes; the host sends the tail to the scalar one).
+// Generated source for prog, or "" with err set. Three kernels: lt_index_kernel (one pixel per
+// thread, any pixel stride), lt_index_kernel4 (four consecutive pixels per thread, vector loads
+// and stores, for 4-aligned planar bands) and lt_index_kernel4i (the same for pixel-interleaved
+// bands); the host sends the tail to the scalar one.
 inline std::string codegen_body(const lt_index_prog& P, bool vec, std::string& err,
                                 std::string& store_out);
 inline std::string codegen(const lt_index_prog& P, std::string& err) {
@@ -127,11 +128,11 @@ inline std::string codegen(const lt_index_prog& P, std::string& err) {
   src += std::string("typedef ") + OT + " lt_ot4 __attribute__((ext_vector_type(4)));\n";
   src += std::string("extern \"C\" __global__ __launch_bounds__(256) void lt_index_kernel(const ") +
          BT + "* __restrict__ bands, long long obs_stride, long long band_stride, long long n_pix, " +
-         OT + "* __restrict__ out, long long out_stride) {\n"
+         OT + "* __restrict__ out, long long out_stride, long long pix_stride) {\n"
          "  const long long p = (long long)blockIdx.x * 256 + threadIdx.x;\n"
          "  const long long o = blockIdx.y;\n"
          "  if (p >= n_pix) return;\n"
-         "  const " + BT + "* b = bands + o * obs_stride + p;\n";
+         "  const " + BT + "* b = bands + o * obs_stride + p * pix_stride;\n";
   src += body1;
   src += "  out[o * out_stride + p] = " + store1 + ";\n}\n";
   src += std::string("extern \"C\" __global__ __launch_bounds__(256) void lt_index_kernel4(const ") +
@@ -144,6 +145,30 @@ inline std::string codegen(const lt_index_prog& P, std::string& err) {
   for (int s = 0; s < P.n_bands; s++)
     src += "  const lt_bt4 bv" + std::to_string(s) + " = *(const lt_bt4*)(b + " +
            std::to_string(s) + "LL * band_stride);\n";
+  src += "  lt_ot4 res;\n#pragma unroll\n  for (int j = 0; j < 4; j++) {\n";
+  src += body4;
+  src += "  res[j] = " + store4 + ";\n  }\n  *(lt_ot4*)(out + o * out_stride + p) = res;\n}\n";
+  // pixel-interleaved bands (band s of pixel p at p * n_bands + s): a 4-pixel group's n_bands * 4
+  // values are contiguous, read as n_bands 4-element vector loads and regrouped per band
+  const int nb = P.n_bands;
+  src += std::string("extern \"C\" __global__ __launch_bounds__(256) void lt_index_kernel4i(const ") +
+         BT + "* __restrict__ bands, long long obs_stride, long long n_pix, " + OT +
+         "* __restrict__ out, long long out_stride) {\n"
+         "  const long long p = ((long long)blockIdx.x * 256 + threadIdx.x) * 4;\n"
+         "  const long long o = blockIdx.y;\n"
+         "  if (p >= n_pix) return;\n"
+         "  const " + BT + "* b = bands + o * obs_stride + p * " + std::to_string(nb) + "LL;\n";
+  for (int k = 0; k < nb; k++)
+    src += "  const lt_bt4 c" + std::to_string(k) + " = *(const lt_bt4*)(b + " +
+           std::to_string(4 * k) + ");\n";
+  for (int sb = 0; sb < nb; sb++) {
+    src += "  lt_bt4 bv" + std::to_string(sb) + ";\n";
+    for (int j = 0; j < 4; j++) {
+      const int e = j * nb + sb;
+      src += "  bv" + std::to_string(sb) + "[" + std::to_string(j) + "] = c" +
+             std::to_string(e / 4) + "[" + std::to_string(e % 4) + "];\n";
+    }
+  }
   src += "  lt_ot4 res;\n#pragma unroll\n  for (int j = 0; j < 4; j++) {\n";
   src += body4;
   src += "  res[j] = " + store4 + ";\n  }\n  *(lt_ot4*)(out + o * out_stride + p) = res;\n}\n";

@@ -209,8 +209,9 @@ class Engine:
         return IndexFn(fn, program, linear_form(program))
 
     def index_tile(self, fn, bands, out=None, stream=None):
-        """bands: [K, NB, P] band planes (NB = the program's band slots, unit pixel stride) in
-        the program's band type; returns the [K, P] index raster in the program's output type."""
+        """bands: [K, NB, P] band planes (NB = the program's band slots; unit pixel stride, or
+        pixel-interleaved: band stride 1, pixel stride NB) in the program's band type; returns the
+        [K, P] index raster in the program's output type."""
         prog = fn.program
         want = _TORCH_OF_LT[_LT_T_OF_NP(prog.band_dtype)]
         if bands.dim() != 3 or bands.dtype != want or bands.device != self.device:
@@ -219,7 +220,10 @@ class Engine:
         K, NB, P = bands.shape
         if NB != len(prog.bands):
             raise LtError('bands must have %d band planes' % len(prog.bands))
-        if bands.stride(2) != 1:  # pixel-interleaved bands: the load kernel reads planes
+        # planar ([K, NB, P], unit pixel stride) or pixel-interleaved (band stride 1, pixel stride
+        # NB: lt_index_kernel4i reads a 4-pixel group's bands with NB vector loads)
+        inter = bands.stride(1) == 1 and bands.stride(2) == NB and NB > 1
+        if bands.stride(2) != 1 and not inter:
             bands = bands.contiguous()
         odt = _TORCH_OF_LT[_LT_T_OF_NP(prog.out_dtype)]
         if out is None:
@@ -228,7 +232,10 @@ class Engine:
             raise LtError('out must be a %s [K, P] tensor' % odt)
         io = _abi.LtIndexIO()
         io.n_pix, io.n_obs = P, K
-        io.obs_stride, io.band_stride = bands.stride(0), bands.stride(1)
+        # (one band plane: its band stride is never used; the obs stride stands in)
+        io.obs_stride = bands.stride(0)
+        io.band_stride = bands.stride(1) if NB > 1 else bands.stride(0)
+        io.band_pix_stride = bands.stride(2)
         io.out_stride = out.stride(0)
         io.bands, io.out = bands.data_ptr(), out.data_ptr()
         st = stream if stream is not None else torch.cuda.current_stream(self.device)
