@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define LT_ABI_VERSION 4
+#define LT_ABI_VERSION 5
 #define LT_MAX_YEARS 64   /* distinct calendar years per scene (T <= 40 in every config) */
 #define LT_MAX_OBS 1024   /* observations per scene (K*T) */
 #define LT_MAX_RULES 16

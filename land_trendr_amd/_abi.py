@@ -10,7 +10,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, 'liblt_hip.so')
 
-LT_ABI_VERSION = 4
+LT_ABI_VERSION = 5
 LT_MAX_YEARS = 64
 LT_MAX_OBS = 1024
 LT_MAX_RULES = 16
