@@ -231,7 +231,10 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
         const int64_t os2 = in.band_obs_stride >> 1;
         int32_t w[WB];
 #pragma unroll
-        for (int u = 0; u < WB; u++) w[u] = (bw + row_of(u, uni) * os2)[pp];
+        // nontemporal: the band pairs are read once; the x-set table stays L2-hot (c5 +1.4 %,
+        // profiles/r03_ab13)
+        for (int u = 0; u < WB; u++)
+          w[u] = __builtin_nontemporal_load(&(bw + row_of(u, uni) * os2)[pp]);
         const int c0 = (int)(uint32_t)LN.c0, k0 = (int)LN.coef[0], k1 = (int)LN.coef[1];
 #pragma unroll
         for (int u = 0; u < WB; u++) {
