@@ -14,6 +14,7 @@ for C in c4 c2; do
     --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port $P bench.py \
     --gpus 2 --config $C --pixels 4000000 --steps 2 --warmup 1 --no-cpu-baseline --e2e-steps 0 \
     > $O/bench_${C}_n2_gloo.json 2> $O/bench_${C}_n2_gloo.err
-  python -c "import json;d=json.load(open('$O/bench_${C}_n2_gloo.json'));print('$C n2',d['value'],d['n_gpus'],d['config']['parallelism'],d['parity_sample']['mismatched_values'])"
+  grep '^{' $O/bench_${C}_n2_gloo.json > $O/${C}_line.json  # gloo logs share stdout
+  python -c "import json;d=json.load(open('$O/${C}_line.json'));print('$C n2',d['value'],d['n_gpus'],d['config']['parallelism'],d['parity_sample']['mismatched_values'])"
   P=$((P + 1))
 done
