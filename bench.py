@@ -30,6 +30,7 @@ import torch
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+from land_trendr_amd._abi import build_hash  # noqa: E402
 from land_trendr_amd.distributed import Mosaic, TrendlineStream  # noqa: E402
 from land_trendr_amd.engine import get_engine, valid_bytes  # noqa: E402
 from land_trendr_amd.index_eqn import IndexProgram  # noqa: E402
@@ -41,8 +42,28 @@ from land_trendr_amd.synth import make_scene, mosaic_inputs  # noqa: E402
 # MI355X peaks (MI355X_MICROARCH.md)
 FP64_PEAK_TFLOPS = 78.6          # 256 CUs x 4 SIMDs x 16 lanes x 2 (FMA) x 2.4 GHz
 HBM_PEAK_GBS = 8000.0
-SIMDS, CLOCK_GHZ, CYC_PER_VALU = 1024, 2.4, 4
-VALU_PEAK_G = SIMDS * CLOCK_GHZ / CYC_PER_VALU  # 614.4 G wave64 VALU instructions/s
+SIMDS, CLOCK_GHZ = 1024, 2.4
+VALU_PEAK_FILE = os.path.join('profiles', 'r04_valu_peak.json')
+
+
+def valu_peak():
+    """The VALU issue peak the analyze kernel's roofline is priced against: measured on the box
+    by tools/valu_peak.hip (profiles/r04_valu_peak.json) — the chip's wave64 VALU instructions/s
+    for a register-only stream of the c2 analyze kernel's instruction mix (PMC: 21 % FP64, 2 %
+    INT64, the rest 32-bit, half as many SALU) at the kernel's occupancy, 4 waves per SIMD.
+    Returns (G instructions/s, source, details)."""
+    try:
+        with open(os.path.join(ROOT, VALU_PEAK_FILE)) as f:
+            d = json.load(f)
+        by = {(r['kind'], r['waves_per_simd']): r for r in d['results']}
+        mix = by[('mix_c2', 4)]
+        det = {k: round(by[(k, 4)]['cycles_per_valu_simd'], 3)
+               for k in ('add_u32', 'cndmask_b32', 'cmp_gt_u32', 'fma_f32', 'add_f64', 'fma_f64',
+                         'mul_f64', 'rcp_f64', 'lshlrev_b64', 'mix_c2') if (k, 4) in by}
+        return mix['g_valu_per_s_chip'], VALU_PEAK_FILE, det
+    except (OSError, ValueError, KeyError):
+        # not measured: the 4-cycle-per-instruction model (an assumption, flagged in the line)
+        return SIMDS * CLOCK_GHZ / 4, 'model: 4 cycles per wave64 VALU instruction', None
 TARGET = '2014-07-01'
 
 GD = [{'name': 'gd', 'val': 1, 'change_type': 'GD'}]
@@ -85,20 +106,27 @@ def bytes_per_pixel(cfg, n_obs, n_years, fused=True):
     return inp + lab + tl + 4
 
 
-def pmc_summary(config):
-    """The committed rocprofv3 --pmc summary of this build for `config` (profiles/
-    summarize_pmc.py: per-launch counters of one 16.8 Mpx launch; c4 runs c2's kernel instance)."""
+def pmc_summary(config, build):
+    """The committed rocprofv3 --pmc summary for `config` (profiles/summarize_pmc.py:
+    per-launch counters of one 16.8 Mpx launch; c4 runs c2's kernel instance): the one collected
+    on this kernel build (its '_build' equals `build`, _abi.build_hash) if committed, else the
+    newest, whose '_matches_build' is then False and whose counters describe another build."""
     name = {'c4': 'c2'}.get(config, config)
-    for rnd in ('r03', 'r02'):  # the newest summary committed for this config
+    found = []
+    for rnd in ('r04', 'r03', 'r02'):  # newest first
         path = os.path.join(ROOT, 'profiles', '%s_pmc_%s.json' % (rnd, name))
         try:
             with open(path) as f:
                 d = json.load(f)
-            d['_path'] = os.path.relpath(path, ROOT)
-            return d
         except (OSError, ValueError):
             continue
-    return None
+        d['_path'] = os.path.relpath(path, ROOT)
+        d['_matches_build'] = d.get('_build') == build
+        found.append(d)
+    for d in found:
+        if d['_matches_build']:
+            return d
+    return found[0] if found else None
 
 
 def per_px(pmc, kernel, counter):
@@ -396,6 +424,21 @@ def main():
                    'checker': 'oracle/lt_oracle.c on a seeded sample of each rank\'s pixels, '
                               'from the index rasters of the bands the timed steps read '
                               '(lt_index_apply)'}
+    # the exchange (N > 1): every label tile the writer received equals the owner's copy,
+    # compared as per-(tile, field) position-weighted byte sums all-reduced to every rank
+    xcheck = None
+    if gather:
+        ex = runner.exchange
+        own = ex.checksums(mosaic.mine)
+        tot = own.to(dev)
+        dist.all_reduce(tot)  # each tile's sums come from its owner alone
+        if ex.is_writer:
+            got = ex.checksums(mosaic.tiles)
+            bad = int((got.to(dev) != tot).any(dim=1).sum().item())
+            xcheck = {'tiles': len(mosaic.tiles), 'fields': list(ex.fields),
+                      'mismatched_tiles': bad,
+                      'check': 'per-(tile, field) position-weighted byte sums of the writer\'s '
+                               'received label planes vs the owners\' (all-reduced)'}
     # the load kernel alone (its HBM roofline): one tile, serially, after the timed region
     it0 = items[0]
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
@@ -435,13 +478,16 @@ def main():
     my_px = sum(it.tile.n for it in items)
     px_per_launch = my_px * args.steps / n_launch
     meta = items[0].scene
-    pmc = pmc_summary(args.config)
+    build = build_hash()
+    pmc = pmc_summary(args.config, build)
+    peak_g, peak_src, peak_cyc = valu_peak()
     valu_px = per_px(pmc, 'analyze', 'SQ_INSTS_VALU')
     achieved = (valu_px * px_per_launch / (kern_ms * 1e-3) / 1e9) if valu_px else None
     pmc_frac = None
     if pmc and 'GRBM_GUI_ACTIVE' in pmc.get('analyze', {}):
-        a = pmc['analyze']  # clock-free: VALU issue cycles / SIMD cycles of the PMC launch
-        pmc_frac = a['SQ_INSTS_VALU'] * CYC_PER_VALU / (SIMDS * a['GRBM_GUI_ACTIVE'] / 8)
+        a = pmc['analyze']  # the PMC launch alone: its VALU rate against the same peak
+        pmc_ms = a['GRBM_GUI_ACTIVE'] / 8 / (CLOCK_GHZ * 1e6)
+        pmc_frac = a['SQ_INSTS_VALU'] / (pmc_ms * 1e-3) / 1e9 / peak_g
     step_valu = None
     if pmc:
         tot = sum(per_px(pmc, k, 'SQ_INSTS_VALU') or 0.0 for k in ('analyze', 'resolve', 'index'))
@@ -478,19 +524,23 @@ def main():
                                    'to rank 0' % world) if mosaic_cfg else
                                   ('one scene per GPU (%d), labels sent to rank 0' % world)},
         # dominant kernel: analyze (>= 80 % of the GPU time), bound by VALU instruction issue —
-        # not HBM (85 B/px) and not FP64 throughput (22 % of its VALU work is FP64). achieved =
+        # not HBM (85 B/px) and not FP64 throughput (21 % of its VALU work is FP64). achieved =
         # the VALU wave-instructions it issues per launch (PMC SQ_INSTS_VALU per pixel, committed
-        # summary) x pixels per launch / the launch's live HIP-event time; peak = 1024 SIMDs x
-        # 2.4 GHz / 4 cycles per wave64 VALU instruction
-        'roofline': {'bound': 'valu-issue', 'achieved': r(achieved, 2), 'peak': VALU_PEAK_G,
+        # summary of this build) x pixels per launch / the launch's live HIP-event time; peak =
+        # the measured issue rate of a register-only stream of the same instruction mix at the
+        # same occupancy (tools/valu_peak.hip, profiles/r04_valu_peak.json)
+        'roofline': {'bound': 'valu-issue', 'achieved': r(achieved, 2), 'peak': round(peak_g, 2),
                      'unit': 'G VALU wave-instr/s',
-                     'frac': r(achieved / VALU_PEAK_G if achieved else None),
+                     'frac': r(achieved / peak_g if achieved else None),
+                     'peak_source': peak_src, 'cycles_per_valu_at_4_waves': peak_cyc,
+                     'build': build, 'pmc_build': pmc.get('_build') if pmc else None,
+                     'pmc_matches_build': bool(pmc and pmc['_matches_build']),
                      'traffic': None if traffic_px is None else round(traffic_px * px_per_launch),
                      'traffic_source': pmc['_path'] if traffic_px is not None else None,
                      'kernel': 'analyze_fast_kernel', 'kernel_ms': round(kern_ms, 3),
                      'valu_instr_per_px': r(valu_px, 2),
-                     'pmc_valu_issue_frac': r(pmc_frac),  # from the PMC launch alone, clock-free
-                     'step_valu_issue_frac': r(step_valu / VALU_PEAK_G if step_valu else None),
+                     'pmc_valu_issue_frac': r(pmc_frac),  # the PMC launch alone (GRBM cycles at 2.4 GHz)
+                     'step_valu_issue_frac': r(step_valu / peak_g if step_valu else None),
                      'fp64': None if f64_px is None else {
                          'achieved': r(f64_px * px_per_launch / (kern_ms * 1e-3) / 1e12, 3),
                          'peak': FP64_PEAK_TFLOPS, 'unit': 'TFLOP/s',
@@ -506,6 +556,7 @@ def main():
                      'reference_work_equivalent_tflops': round(ref_equiv, 2)},
         'status_numeric_pixels': n_numeric,
         'parity_sample': psample,
+        'exchange_check': xcheck,
         'load_stage': {
             'fused': runner.fused,
             'kernel': ('analyze_fast_kernel (index_eqn "B1 - B2" as lt_index_lin, evaluated on '
@@ -533,6 +584,10 @@ def main():
     if psample is not None and psample['mismatched_values'] != 0:
         print('bench: %d values of the parity sample differ from the oracle'
               % psample['mismatched_values'], file=sys.stderr)
+        sys.exit(3)
+    if xcheck is not None and xcheck['mismatched_tiles'] != 0:
+        print('bench: %d exchanged label tiles differ from their owners\' planes'
+              % xcheck['mismatched_tiles'], file=sys.stderr)
         sys.exit(3)
 
 

@@ -56,6 +56,29 @@ class LtScene(ctypes.Structure):
                 ('feb29_bad', c_u8p)]
 
 
+def build_hash():
+    """Identity of the kernel build: sha256 (first 16 hex digits) over the sources liblt_hip.so
+    is compiled from (csrc/*.h, csrc/*.hip, include/lt_abi.h) and the compile flags. bench.py
+    records it in its line and profiles/summarize_pmc.py in every PMC summary, so a roofline
+    whose counters come from another build is flagged."""
+    import hashlib
+    csrc = os.path.join(HERE, 'csrc')
+    files = sorted(os.path.join(csrc, f) for f in os.listdir(csrc)
+                   if f.endswith(('.h', '.hip')))
+    files.append(os.path.join(os.path.dirname(HERE), 'include', 'lt_abi.h'))
+    h = hashlib.sha256()
+    for f in files:
+        h.update(os.path.basename(f).encode() + b'\0')
+        with open(f, 'rb') as fh:
+            h.update(fh.read())
+    try:
+        import __graft_entry__ as ge  # the flags the library is built with
+        h.update(' '.join(ge.HIP_FLAGS).encode())
+    except ImportError:
+        pass
+    return h.hexdigest()[:16]
+
+
 LT_LIN_MAX_BANDS = 4
 
 

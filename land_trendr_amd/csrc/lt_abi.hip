@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <map>
@@ -475,7 +476,16 @@ int lt_analyze_tiles_after(lt_ctx* c, const lt_scene* sc, const lt_params* prm, 
     c->defer_cap = cap;
   }
   if (!c->side) {
-    HIP_OR_FAIL(c, hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+    // the resolve stage's stream has the lowest priority: its few long, latency-bound waves then
+    // take CU slots only when the next tile's analyze waves leave them (the drain of a launch),
+    // instead of displacing them at the launch's start (kernel trace r04_run1: a resolve launch
+    // that got its slots first cost the analyze launch beside it 0.25-0.29 ms; one that did not
+    // ran in its shadow for free). LT_RESOLVE_PRIORITY=normal keeps the default (A/B runs).
+    int least = 0, greatest = 0;
+    HIP_OR_FAIL(c, hipDeviceGetStreamPriorityRange(&least, &greatest));
+    const char* pr = getenv("LT_RESOLVE_PRIORITY");
+    const bool normal = pr && strcmp(pr, "normal") == 0;
+    HIP_OR_FAIL(c, hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, normal ? 0 : least));
     for (int s = 0; s < 2; s++) {
       HIP_OR_FAIL(c, hipEventCreateWithFlags(&c->ev_analyzed[s], hipEventDisableTiming));
       HIP_OR_FAIL(c, hipEventCreateWithFlags(&c->ev_resolved[s], hipEventDisableTiming));

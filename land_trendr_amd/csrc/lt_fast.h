@@ -226,7 +226,9 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
       const lt_index_lin& LN = in.lin;
       const int nb = LN.n_bands;
       int32_t acc[WB];  // the sum modulo 2^32: a 24-bit multiply-add per band
-      if (nb == 2 && in.band_stride == 1) {  // a pixel-interleaved pair: one 32-bit load
+      // a pixel-interleaved pair: one 32-bit load (check_tile: 4-byte aligned, even obs stride).
+      // A planar tile of one pixel may also have band_stride 1: not a pair
+      if (nb == 2 && in.band_stride == 1 && in.band_pix_stride == 2) {
         const int32_t* bw = (const int32_t*)in.obs_bands;
         const int64_t os2 = in.band_obs_stride >> 1;
         int32_t w[WB];

@@ -126,10 +126,20 @@ class LabelExchange:
             self._slabs = {t.t: {f: torch.empty(shape(f), dtype=self.spec[f][1],
                                                 device=self.device) for f in self.fields}
                            for t in mosaic.mine}
+        # gloo (the 1-GPU rehearsals and the GPU tests' multi-rank runs) hands a tensor's data
+        # pointer to its CPU transport, which for a device tensor would read HBM without waiting
+        # for the kernels that write it: device slabs then travel through host copies (the sender
+        # copies after its queued work, the writer copies in after the receive). RCCL ops are
+        # stream-ordered and take the device slabs directly.
+        self._staged = (mosaic.world > 1 and self.device.type == 'cuda' and
+                        dist.get_backend() == 'gloo')
+        self._staged_in = []   # (host buffer, device slab) pairs to copy in after wait()
+        self._staged_out = []  # host copies of sent slabs, kept alive until wait()
         # the writer's receives wait for nothing it computes: they are posted from a stream of
         # their own (an RCCL op first waits for the work queued on the current stream)
         self._recv_stream = (torch.cuda.Stream(self.device)
-                             if self.is_writer and self.device.type == 'cuda' else None)
+                             if self.is_writer and self.device.type == 'cuda' and not self._staged
+                             else None)
         self._works = []
 
     def slab(self, tile):
@@ -148,12 +158,23 @@ class LabelExchange:
                 mine = self.m.tiles_of(r)
                 if k < len(mine):
                     t = mine[k].t
-                    ops += [d.P2POp(d.irecv, self.full[f][t], r) for f in self.fields]
+                    for f in self.fields:
+                        dst = self.full[f][t]
+                        if self._staged:
+                            buf = torch.empty(dst.shape, dtype=dst.dtype)
+                            self._staged_in.append((buf, dst))
+                            dst = buf
+                        ops.append(d.P2POp(d.irecv, dst, r))
         else:
             mine = self.m.mine
             if k < len(mine):
                 s = self._slabs[mine[k].t]
-                ops += [d.P2POp(d.isend, s[f], self.dst) for f in self.fields]
+                for f in self.fields:
+                    src = s[f]
+                    if self._staged:  # a blocking copy: after the kernels queued so far
+                        src = src.cpu()
+                        self._staged_out.append(src)
+                    ops.append(d.P2POp(d.isend, src, self.dst))
         if ops:
             if self._recv_stream is not None:
                 with torch.cuda.stream(self._recv_stream):
@@ -168,6 +189,22 @@ class LabelExchange:
     def wait(self):
         while self._works:
             self._works.pop(0).wait()
+        for buf, dst in self._staged_in:
+            dst.copy_(buf)
+        self._staged_in, self._staged_out = [], []
+
+    def checksums(self, tiles):
+        """Position-weighted byte sums, one per (tile, field), of the slabs of `tiles` as this
+        rank holds them: the writer's copies of every tile, a sender's own. Comparing the writer's
+        with the owners' checks every exchanged byte landed where it belongs."""
+        out = torch.zeros((len(self.m.tiles), len(self.fields)), dtype=torch.int64)
+        for t in tiles:
+            for j, f in enumerate(self.fields):
+                a = (self.full[f][t.t] if self.is_writer else self._slabs[t.t][f])[..., :t.n]
+                b = a.contiguous().view(torch.uint8).reshape(-1).to(torch.int64)
+                w = torch.arange(b.numel(), device=b.device, dtype=torch.int64) % 251 + 1
+                out[t.t, j] = int((b * w).sum().item())
+        return out
 
     def raster(self, field):
         """[rows, n_pix] (or [n_pix]) in mosaic pixel order (writer only): the tile-major slabs
@@ -215,7 +252,9 @@ class TrendlineStream:
 
     def push(self, planes, n=None, key=None):
         """Queue the D2H of every row of planes[f] ([rows, W] device tensors; the first n pixels
-        of each row, all W by default) after the work queued so far on the current stream."""
+        of each row, all W by default) after the work queued so far on the current stream.
+        Returns an event recorded after the last of these copies: the planes may be overwritten
+        once it has completed."""
         ready = torch.cuda.Event()
         ready.record()
         self.stream.wait_event(ready)
@@ -237,6 +276,9 @@ class TrendlineStream:
                 self.pending[slot] = (ev, f, r, nb, key)
                 self.count += 1
                 self.bytes += nb
+        done = torch.cuda.Event()
+        done.record(self.stream)
+        return done
 
     def drain(self):
         for k in range(len(self.ring)):

@@ -279,31 +279,49 @@ class _Offsets:
         return hit
 
 
-def ingest_stack(rast_fns, grid, mask_fns=None, bands=None, threads=None):
+def ingest_stack(rast_fns, grid, mask_fns=None, bands=None, threads=None, pixels=None):
     """parse_mapper over every analysis raster, as planes for analysis_reducer_batch.
 
     rast_fns: the (decompressed) analysis rasters, in the mapper order that becomes each pixel's
     observation order; grid: CSV path, WKT list or (lng, lat) arrays (P points); mask_fns: per
     raster the mask path or None (default: mask_name(fn) when that file exists); bands: the band
     numbers to gather (default: all bands of each raster); threads: decode / gather workers
-    (default host_threads(): the codecs and the gathers release the GIL).
-    Returns dict(dates=['YYYY-MM-DD'] * K, bands=[K, nb, P] in the rasters' sample type,
-    band_numbers=[nb], valid=[K, P] uint8)."""
+    (default host_threads(): the codecs and the gathers release the GIL); pixels: None (every
+    grid point) or a list of grid-point ranges [(p0, p1), ...] — a rank's tiles of a multi-rank
+    job — whose samples alone are gathered, back to back, so a rank holds 1/N of the stack's
+    planes (the reference shards parse_mapper per raster, mr_land_trendr_job.py:45-81; here each
+    rank keeps the pixel columns its tiles analyse).
+    Returns dict(dates=['YYYY-MM-DD'] * K, bands=[K, nb, Q] in the rasters' sample type,
+    band_numbers=[nb], valid=[K, Q] uint8, n_pix=P, ranges=[(p0, p1, q0)]) with Q the points
+    gathered; grid point p of range (p0, p1, q0) is column q0 + p - p0 (stack_range)."""
     from concurrent.futures import ThreadPoolExecutor
     lng, lat = grid if isinstance(grid, tuple) else grid_points(grid)
     P = len(lng)
     K = len(rast_fns)
+    if pixels is None:
+        pixels = [(0, P)] if P else []
+    ranges, q = [], 0
+    for p0, p1 in pixels:
+        if not 0 <= p0 <= p1 <= P:
+            raise ValueError('pixel range (%d, %d) outside the grid of %d points' % (p0, p1, P))
+        ranges.append((int(p0), int(p1), q))
+        q += p1 - p0
+    Q = q
+    if len(ranges) != 1 or ranges[0][:2] != (0, P):
+        sel_pts = (np.concatenate([np.arange(a, b) for a, b, _ in ranges]) if ranges
+                   else np.zeros(0, np.int64))
+        lng, lat = lng[sel_pts], lat[sel_pts]
     if mask_fns is None:
         mask_fns = [mask_name(f) if os.path.exists(mask_name(f)) and mask_name(f) != f else None
                     for f in rast_fns]
     if K == 0:
-        return dict(dates=[], bands=np.zeros((0, 0, P)), band_numbers=list(bands or []),
-                    valid=np.zeros((0, P), np.uint8), n_pix=P)
+        return dict(dates=[], bands=np.zeros((0, 0, Q)), band_numbers=list(bands or []),
+                    valid=np.zeros((0, Q), np.uint8), n_pix=P, ranges=ranges)
     first = _open(rast_fns[0])
     numbers = list(bands) if bands is not None else list(range(1, first.bands + 1))
     dtype = first.dtype.newbyteorder('=')
-    out_bands = np.empty((K, len(numbers), P), dtype)
-    valid = np.empty((K, P), np.uint8)
+    out_bands = np.empty((K, len(numbers), Q), dtype)
+    valid = np.empty((K, Q), np.uint8)
     offsets = _Offsets(lng, lat)
     sel = [b - 1 for b in numbers]
 
@@ -335,4 +353,15 @@ def ingest_stack(rast_fns, grid, mask_fns=None, bands=None, threads=None):
     n = max(1, min(K, threads or host_threads()))
     with ThreadPoolExecutor(n) as pool:
         dates = list(pool.map(one, range(K)))
-    return dict(dates=dates, bands=out_bands, band_numbers=numbers, valid=valid, n_pix=P)
+    return dict(dates=dates, bands=out_bands, band_numbers=numbers, valid=valid, n_pix=P,
+                ranges=ranges)
+
+
+def stack_range(stack, p0, p1):
+    """The (bands [K, nb, n], valid [K, n]) views of grid points p0..p1 of an ingest_stack
+    result: they must lie inside one of the ranges it gathered."""
+    for a, b, q0 in stack.get('ranges', [(0, stack['n_pix'], 0)]):
+        if a <= p0 and p1 <= b:
+            q = q0 + p0 - a
+            return stack['bands'][:, :, q:q + p1 - p0], stack['valid'][:, q:q + p1 - p0]
+    raise KeyError('grid points %d..%d were not gathered by this rank' % (p0, p1))

@@ -39,7 +39,7 @@ import numpy as np
 
 from . import _abi
 from .ingest import (analysis_rasters, grid_coords, grid_offsets, ingest_stack, mask_name,
-                     rast2grid, rast_local, read_grid)
+                     rast2grid, rast_local, read_grid, stack_range)
 
 IN_SETTINGS = '%s/input/settings.json'
 IN_RASTS = '%s/input/rasters/'
@@ -122,9 +122,17 @@ class LocalJob:
 
     # 2. parse_mapper
     def parse(self):
+        """Band samples and mask validity of the grid points of this rank's tiles only (the tiles
+        of the grid dealt round-robin over the ranks, as analyze runs them): a rank's host planes
+        and gathers are 1/N of the job's."""
+        from .distributed import Mosaic
         from .index_eqn import parse_eqn_bands
+        _, world, rank = self._dist()
+        P = len(self.grid_xy[0])
+        self.mosaic = Mosaic([P], self.tile_pixels, world, rank, 'round_robin')
         eqn_bands = sorted(parse_eqn_bands(self.settings['index_eqn']))
-        self.stack = ingest_stack(self.rast_fns, self.grid_xy, self.mask_fns, bands=eqn_bands)
+        self.stack = ingest_stack(self.rast_fns, self.grid_xy, self.mask_fns, bands=eqn_bands,
+                                  pixels=[(t.p0, t.p1) for t in self.mosaic.mine])
         return self.stack
 
     # 3. analysis_reducer, batched over pixel tiles: the mosaic path (runner.py) bench.py runs
@@ -133,10 +141,11 @@ class LocalJob:
         initialised), analysed by runner.MosaicRunner. The label planes (and status / n_years) go
         to rank 0, the writer, through the LabelExchange; the per-year trendline planes leave the
         GPU per tile, while the next tile computes, into host planes [Y, P] (file-backed maps in
-        work_dir, shared by the ranks, when there are several): no GPU ever holds the whole
-        job's trendline. Returns the writer's label planes (device), None on the other ranks."""
+        work_dir, shared by the ranks, when there are several), from a ring of three tiles'
+        device buffers: no GPU ever holds more than three tiles of trendline. Returns the
+        writer's label planes (device), None on the other ranks."""
         import torch
-        from .distributed import Mosaic, TrendlineStream
+        from .distributed import TrendlineStream
         from .engine import LABELS, TRENDLINE, get_engine, pack_valid_bits
         from .index_eqn import IndexProgram
         from .runner import MosaicRunner, TileInput
@@ -162,37 +171,45 @@ class LocalJob:
                             raster_count=max(numbers))
         slots = [numbers.index(b) for b in prog.bands]  # the planes the equation reads
         fn = eng.compile_index(prog)
-        m = Mosaic([P], self.tile_pixels, world, rank, 'round_robin')
+        m = self.mosaic
+        if (m.world, m.rank, m.scene_pixels) != (world, rank, [P]):
+            raise RuntimeError('parse() ran under another process group')
         K, Y = self.scene.n_obs, self.scene.n_years
         items = []
         for t in m.mine:
-            bands = torch.from_numpy(np.ascontiguousarray(
-                st['bands'][:, slots, t.p0:t.p1])).to(dev)
+            t_bands, t_valid = stack_range(st, t.p0, t.p1)
+            bands = torch.from_numpy(np.ascontiguousarray(t_bands[:, slots])).to(dev)
             if cuda and fn.lin is not None and len(slots) == 2 and bands.dtype == torch.int16:
                 # the fused load stage reads a pixel's two int16 bands as one 32-bit word
                 inter = torch.empty((K, t.n, 2), dtype=bands.dtype, device=dev).permute(0, 2, 1)
                 inter.copy_(bands)
                 bands = inter
-            valid = torch.from_numpy(np.ascontiguousarray(st['valid'][:, t.p0:t.p1])).to(dev)
+            valid = torch.from_numpy(np.ascontiguousarray(t_valid)).to(dev)
             if cuda:  # the winner pick reads the mask as bit planes (one word per 32 obs)
                 valid = pack_valid_bits(valid)
-            vals = torch.empty((K, t.n), dtype=bands.dtype, device=dev)
-            items.append(TileInput(t, self.scene, vals, valid, bands))
+            # the index raster: allocated by the runner only if the load kernel writes it (the
+            # fused load stage never does)
+            items.append(TileInput(t, self.scene, None, valid, bands))
         host = self.host_trendline = self._trendline_planes(tl_fields, Y, P, dist, world, rank)
+        # the trendline planes: a ring of three tiles' buffers on the GPU (tile k reuses tile
+        # k-3's once its rows have reached the host), so a rank's HBM never holds all its tiles'
+        # trendlines
         runner = MosaicRunner(eng, m, params, items, label_fields + tl_fields, fn, dist,
-                              exchange_fields=label_fields)
+                              exchange_fields=label_fields, ring=3 if cuda else 0)
 
         def sink(f, row, view, t):  # one completed year row of tile t
             host[f][row, t.p0:t.p1] = view.numpy().view(host[f].dtype)
 
         tls = TrendlineStream(m.tile * 8, dev, depth=16, sink=sink) if cuda else None
+        copied = {}  # tile -> event after its rows' D2H copies
 
         def push(k):
             t = items[k].tile
-            tls.push({f: runner.outs[k][f] for f in tl_fields}, t.n, t)
+            copied[k] = tls.push({f: runner.outs[k][f] for f in tl_fields}, t.n, t)
 
         # tile k-1's rows are queued behind tile k's kernels, so the copies overlap them
-        runner.step(after_tile=(lambda k: push(k - 1) if k > 0 else None) if cuda else None)
+        runner.step(after_tile=(lambda k: push(k - 1) if k > 0 else None) if cuda else None,
+                    slab_free=copied.get if cuda else None)
         if cuda:
             if items:
                 push(len(items) - 1)

@@ -33,7 +33,9 @@ _nullctx = contextlib.nullcontext
 class TileInput:
     tile: object                       # distributed.Tile
     scene: object                      # scene.SceneMeta (lt_scene of the tile's scene)
-    values: torch.Tensor               # [K, n] index raster (written by the load stage if bands)
+    # [K, n] index raster: given, or written by the load stage from the bands (None: allocated
+    # when the load kernel first writes it — never, on the fused path)
+    values: Optional[torch.Tensor]
     valid: Optional[torch.Tensor]      # [K, n] uint8 or None
     bands: Optional[torch.Tensor] = None  # [K, NB, n] band planes, or None (values given)
 
@@ -44,11 +46,15 @@ class MosaicRunner:
     fields: the output planes the kernels write per tile; label fields in `exchange_fields` live
     in the LabelExchange's slabs (their final place on the writer rank), the others in per-tile
     slabs of this rank. group: tiles per lt_analyze_tiles call (0: every consecutive tile of a
-    scene, or 1 when labels are exchanged, so tile t's sends travel while tile t+1 computes)."""
+    scene, or 1 when labels are exchanged, so tile t's sends travel while tile t+1 computes).
+    ring: 0, every tile has planes of its own for the fields not exchanged (the trendline
+    planes); R > 0, tile k writes them into buffer k % R of a ring (one tile per call), and
+    step()'s slab_free(j) names the event after which tile j's buffer may be overwritten (its
+    D2H copies done): the rank's HBM then holds R tiles' trendline planes, not all of them."""
 
     def __init__(self, engine, mosaic, params, items, fields, index_fn=None, dist=None,
                  exchange_fields=LABEL_GATHER_FIELDS, load_stream=True, group=0, dst=0,
-                 fused=None):
+                 fused=None, ring=0):
         self.eng, self.m, self.params, self.items = engine, mosaic, params, list(items)
         self.fields = tuple(fields)
         self.index_fn = index_fn
@@ -66,17 +72,22 @@ class MosaicRunner:
         self.exchange = LabelExchange(mosaic, {f: (rows(f), _DTYPE[f]) for f in ex},
                                       engine.device, dist, dst)
         W = mosaic.tile
+        self.ring = max(0, int(ring))
+
+        def planes():
+            return {f: torch.empty((W,) if rows(f) is None else (rows(f), W), dtype=_DTYPE[f],
+                                   device=engine.device) for f in self.fields if f not in ex}
+
+        shared = [planes() for _ in range(min(self.ring, len(self.items)))]
         self.outs = []
-        for it in self.items:
+        for k, it in enumerate(self.items):
             o = dict(self.exchange.slab(it.tile))
-            for f in self.fields:
-                if f not in o:
-                    r = rows(f)
-                    o[f] = torch.empty((W,) if r is None else (r, W), dtype=_DTYPE[f],
-                                       device=engine.device)
+            o.update(shared[k % self.ring] if self.ring else planes())
             self.outs.append(o)
         gathering = mosaic.world > 1 and bool(ex)
         self.group = group if group > 0 else (1 if gathering else 1 << 30)
+        if self.ring:
+            self.group = 1
         has_bands = any(it.bands is not None for it in self.items)
         if has_bands and index_fn is None:
             raise ValueError('band inputs need a compiled index_eqn (index_fn)')
@@ -106,15 +117,19 @@ class MosaicRunner:
         if g:
             yield g
 
-    def step(self, timed=False, after_tile=None, stage_in=None):
+    def step(self, timed=False, after_tile=None, stage_in=None, slab_free=None):
         """Queue one pass over this rank's tiles and complete the label exchange.
         after_tile(k): called once tile k's kernels are queued (e.g. to stream its trendline).
         stage_in: an object whose fetch(k) -> (bands, event) supplies tile k's band planes from
         elsewhere (an H2D copy the load kernel waits for) and whose consumed(k, event) learns
-        when the load kernel has read them."""
+        when the load kernel has read them. slab_free(j): with a ring, the event (or None)
+        after which tile j's ring buffer is free again; tile j + ring waits for it."""
         eng = self.eng
         if not self.cuda:
             timed = False
+        if self.ring and self.cuda and slab_free is None:
+            raise ValueError('a ring of output buffers needs slab_free')
+        self._slab_free = slab_free
         if self.fused:
             return self._step_fused(after_tile, stage_in)
         main = torch.cuda.current_stream(eng.device) if self.cuda else None
@@ -135,7 +150,7 @@ class MosaicRunner:
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(
                         enable_timing=True)
                     e0.record()
-                eng.index_tile(self.index_fn, bands, out=it.values)
+                it.values = eng.index_tile(self.index_fn, bands, out=it.values)
                 if timed:
                     e1.record()
                     self.index_events.append((e0, e1))
@@ -148,6 +163,7 @@ class MosaicRunner:
         for g in self._groups():
             scene = self.items[g[0]].scene
             n = [self.items[k].tile.n for k in g]
+            self._wait_ring(g[0])
             eng.analyze_tiles(
                 scene, self.params, [(self.items[k].values, self.items[k].valid) for k in g],
                 self.fields, outs=[{f: x[..., :nk] for f, x in self.outs[k].items()}
@@ -182,6 +198,7 @@ class MosaicRunner:
                     bands, ev_in = stage_in.fetch(k)
                     ready = [ev_in]
                 tiles.append((bands, self.items[k].valid))
+            self._wait_ring(g[0])
             eng.analyze_tiles(
                 scene, self.params, tiles, self.fields,
                 outs=[{f: x[..., :nk] for f, x in self.outs[k].items()} for k, nk in zip(g, n)],
@@ -198,12 +215,22 @@ class MosaicRunner:
             self.exchange.post(k)
         self.exchange.wait()
 
+    def _wait_ring(self, k):
+        """Tile k reuses the ring buffer of tile k - ring: the current stream waits until that
+        tile's planes have been copied out."""
+        if not self.ring or not self.cuda or k < self.ring:
+            return
+        ev = self._slab_free(k - self.ring)
+        if ev is not None:
+            torch.cuda.current_stream(self.eng.device).wait_event(ev)
+
     def materialise_index(self, k):
         """Tile k's index raster (items[k].values) from its band planes with the load kernel, on
         the current stream — what the fused steps never write; the oracle checks read it."""
-        if self.index_fn is None or self.items[k].bands is None:
+        it = self.items[k]
+        if self.index_fn is None or it.bands is None:
             return
-        self.eng.index_tile(self.index_fn, self.items[k].bands, out=self.items[k].values)
+        it.values = self.eng.index_tile(self.index_fn, it.bands, out=it.values)
 
     def index_ms(self):
         ev, self.index_events = self.index_events, []

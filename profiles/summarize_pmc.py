@@ -42,6 +42,10 @@ def main(root, out, px=None, input_mode='bands'):
         row['launches'] = n
         res[name] = row
     res['_source'] = root
+    # the kernel build the counters belong to (bench.py compares it with its own)
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from land_trendr_amd._abi import build_hash
+    res['_build'] = build_hash()
     res['_pixels_per_launch'] = px
     res['_input'] = input_mode
     json.dump(res, open(out, 'w'), indent=1, sort_keys=True)

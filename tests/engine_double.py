@@ -16,8 +16,11 @@ class OracleEngine:
     def index_tile(self, fn, bands, out=None, stream=None):
         from oracle import index_oracle
         b = bands.numpy()
-        v = index_oracle.evaluate(fn.program, np.moveaxis(b, 1, 0))
-        out.copy_(torch.from_numpy(np.ascontiguousarray(v)))
+        v = torch.from_numpy(np.ascontiguousarray(
+            index_oracle.evaluate(fn.program, np.moveaxis(b, 1, 0))))
+        if out is None:
+            return v
+        out.copy_(v)
         return out
 
     def analyze_tiles(self, scene, params, tiles, fields, outs=None, ready=None):

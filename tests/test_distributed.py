@@ -50,7 +50,11 @@ def _worker(rank, world, port, scene_px, tile, assign, result_path, dst=0):
     os.environ['MASTER_PORT'] = str(port)
     dist.init_process_group('gloo', rank=rank, world_size=world)
     r = _run(world, rank, scene_px, tile, assign, 7, dist, dst)
+    # bench.py's exchange check: the owners' per-tile checksums, all-reduced, equal the writer's
+    tot = r.exchange.checksums(r.m.mine)
+    dist.all_reduce(tot)
     if rank == dst:
+        assert torch.equal(r.exchange.checksums(r.m.tiles), tot)
         np.savez(result_path, **{f: r.exchange.raster(f).numpy()
                                  for f in ltd.LABEL_GATHER_FIELDS})
     dist.barrier()
@@ -133,6 +137,12 @@ def _job_worker(rank, world, port, root, result_path):
     dist.init_process_group('gloo', rank=rank, world_size=world)
     j = LocalJob(root, 'synth', tile_pixels=20, on_error='skip', engine=OracleEngine())
     files = j.run()
+    # this rank's parse gathered only the grid points of its own tiles
+    st = j.stack
+    np.savez('%s.rank%d.npz' % (result_path, rank), bands=st['bands'], valid=st['valid'],
+             ranges=np.array(st['ranges'], np.int64).reshape(-1, 3),
+             mine=np.array([(t.p0, t.p1) for t in j.mosaic.mine], np.int64).reshape(-1, 2),
+             n_pix=st['n_pix'])
     if rank == 0:
         arrs = {'raster:' + k: GeoTiff(v[0]).read() for k, v in files.items()}
         arrs.update({'plane:' + k: a for k, a in j.planes.items()})
@@ -168,6 +178,20 @@ def test_multi_rank_job_matches_single_rank_and_oracle(tmp_path):
     for k, v in files.items():
         assert np.array_equal(GeoTiff(v[0]).read(), got['raster:' + k]), k
     st = j.stack
+    # per-rank ingest: each rank's stack holds its own tiles' grid points only (about half of
+    # them here), and they are the single-rank stack's columns of those points
+    held = 0
+    for rank in range(2):
+        r = np.load('%s.rank%d.npz' % (path, rank))
+        assert int(r['n_pix']) == st['n_pix']
+        assert [tuple(x[:2]) for x in r['ranges']] == [tuple(x) for x in r['mine']]
+        n = int((r['mine'][:, 1] - r['mine'][:, 0]).sum())
+        assert r['bands'].shape[-1] == n == r['valid'].shape[-1] < st['n_pix']
+        for p0, p1, q0 in r['ranges']:
+            assert np.array_equal(r['bands'][:, :, q0:q0 + p1 - p0], st['bands'][:, :, p0:p1])
+            assert np.array_equal(r['valid'][:, q0:q0 + p1 - p0], st['valid'][:, p0:p1])
+        held += n
+    assert held == st['n_pix']
     idx = (st['bands'][:, 0, :].astype(np.int32) - st['bands'][:, 1, :]).astype(np.int16)
     meta = build_scene(st['dates'], parse_date(SETTINGS['target_date']))
     params, _ = compile_params(SETTINGS['line_cost'], SETTINGS['label_rules'])

@@ -249,3 +249,27 @@ def test_fused_load_stage_matches_index_raster_path(engine, eqn, bt, ot, masked)
         w, g = want[f].cpu().numpy(), got[f].cpu().numpy()
         same = _bits_equal(w, g)
         assert same.all(), '%s %s: %s differs in %d places' % (eqn, bt, f, (~same).sum())
+
+
+def test_fused_load_stage_one_pixel_planar_band_slice(engine):
+    """A planar one-pixel tile whose two int16 bands are a slice of a 3-band stack ([K, 3, 1]
+    viewed as bands 1:3: band stride 1, pixel stride 1, data 2 bytes off a 4-byte boundary, obs
+    stride 3) is not a pixel-interleaved pair: the fused kernel reads it band by band and writes
+    what the index-raster path writes (it used to take the 32-bit pair load)."""
+    from land_trendr_amd.engine import ALL_FIELDS
+    from land_trendr_amd.synth import make_scene
+    sc = make_scene(1, seed=5, n_years=30, with_bands=True)
+    K = sc.bands.shape[0]
+    stack = torch.zeros((K, 3, 1), dtype=torch.int16)
+    stack[:, 1:3] = sc.bands
+    b = stack.to(engine.device)[:, 1:3]
+    assert b.stride() == (3, 1, 1) and b.data_ptr() % 4 == 2
+    meta = build_scene(sc.dates, parse_date('2014-07-01'))
+    params, _ = compile_params(10.0, [{'name': 'gd', 'val': 1, 'change_type': 'GD'}])
+    fn = engine.compile_index(index_eqn.IndexProgram('B1 - B2', band_dtype=np.int16))
+    want = engine.analyze_tile(meta, params, engine.index_tile(fn, b), None, ALL_FIELDS)
+    got = engine.analyze_tile(meta, params, b, None, ALL_FIELDS, lin=fn.lin)
+    torch.cuda.synchronize()
+    assert int(want['n_years'][0]) == 30
+    for f in ALL_FIELDS:
+        assert _bits_equal(want[f].cpu().numpy(), got[f].cpu().numpy()).all(), f

@@ -89,3 +89,56 @@ def test_local_job_raises_like_the_reference(tmp_path):
     make_job(root, settings=s)
     with pytest.raises(AttributeError):
         LocalJob(root, 'synth', device=0).run()
+
+
+def _gpu_job_worker(rank, world, port, root, result_path):
+    """One rank of a multi-rank GPU job (every rank on cuda:0; gloo carries the label tiles)."""
+    import torch
+    import torch.distributed as dist
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    j = LocalJob(root, 'synth', device=0, tile_pixels=10, on_error='skip')
+    files = j.run()
+    if rank == 0:
+        arrs = {'raster:' + k: GeoTiff(v[0]).read() for k, v in files.items()}
+        arrs.update({'plane:' + k: a for k, a in j.planes.items()})
+        np.savez(result_path, **arrs)
+    else:
+        assert files is None
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_multi_rank_gpu_job_matches_single_rank(tmp_path):
+    """The default GPU job path over 2 ranks on one GPU (gloo for the label exchange): fused
+    'B1 - B2' load stage, mask bit planes, per-rank ingest, trendline rows streamed by
+    TrendlineStream from a ring of three tiles' buffers into the ranks' shared host maps (tiles of
+    10 px: six tiles per rank, nonzero offsets, every ring buffer reused). Every output raster and
+    plane equals the single-rank GPU job's (the multi-rank job had CPU-only tests)."""
+    import socket
+    import torch.multiprocessing as mp
+    multi, single = str(tmp_path / 'multi'), str(tmp_path / 'single')
+    make_job(multi)
+    make_job(single)
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    path = str(tmp_path / 'job.npz')
+    mp.spawn(_gpu_job_worker, args=(2, port, multi, path), nprocs=2, join=True)
+    got = dict(np.load(path))
+    j = LocalJob(single, 'synth', device=0, tile_pixels=1 << 20, on_error='skip')
+    files = j.run()
+    assert sorted('raster:' + k for k in files) == sorted(k for k in got if k.startswith('raster:'))
+    assert any(k.startswith('trendline/') for k in files)
+    for k, v in files.items():
+        assert np.array_equal(GeoTiff(v[0]).read(), got['raster:' + k]), k
+    m = j.planes['matched'].astype(bool)
+    for k, a in j.planes.items():
+        b = got['plane:' + k]
+        if k in ('onset_year', 'duration', 'class_val', 'magnitude', 'initial_val'):
+            a, b = np.where(m[:a.shape[0]], a, 0), np.where(m[:a.shape[0]], b, 0)
+        assert (_bits_equal(a, b).all() if a.dtype.kind == 'f' else np.array_equal(a, b)), k

@@ -53,14 +53,21 @@ def _bench_runner(cfg_name, fields, pixels=0):
     return MosaicRunner(eng, m, params, items, fields, fn), params
 
 
-@pytest.mark.parametrize('cfg', ['c2', 'c3', 'c4', 'c5'])
+@pytest.mark.parametrize('cfg', ['c2', 'c3', 'c4', 'c5', 'c2-bench', 'c3-bench'])
 def test_bench_path_full_size_sampled_vs_oracle(cfg):
+    """'c2' / 'c3' add the val_fit / vertex planes (the emulated-fit, year-major output path);
+    'c2-bench' / 'c3-bench' request exactly bench.py's fields (labels only), so the kernel
+    instance bench.py times runs: the certified labels path (lt_fast.h LT_CERT_RULES) over an
+    int16 series with the fused 'B1 - B2' load stage, 1 rule (c2) or 3 rules with onset / duration
+    / pre_threshold filters over mask bit planes (c3), on one full 16.8 Mpx tile each."""
     from oracle import oracle
+    bench_fields = cfg.endswith('-bench')
+    cfg = cfg.split('-')[0]
     c = bench.CONFIGS[cfg]
     fields = ['status', 'matched', 'class_val', 'onset_year', 'duration', 'magnitude']
     if cfg == 'c5':
         fields += bench.TRENDLINE_FIELDS
-    elif cfg != 'c4':
+    elif cfg != 'c4' and not bench_fields:
         fields += ['val_fit', 'vertex']
     runner, params = _bench_runner(cfg, fields)
     runner.step()

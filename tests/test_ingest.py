@@ -154,6 +154,19 @@ def test_grid_coords_equal_parsing_the_written_grid(tmp_path):
     st1 = ingest.ingest_stack(j.rast_fns, j.grid_fn, j.mask_fns, bands=[1, 2], threads=1)
     assert st['dates'] == st1['dates']
     assert np.array_equal(st['bands'], st1['bands']) and np.array_equal(st['valid'], st1['valid'])
+    # a rank's share (pixel ranges): exactly those columns, back to back; stack_range finds them
+    P = st['n_pix']
+    spans = [(0, 7), (P // 2, P // 2 + 13), (P - 5, P)]
+    sub = ingest.ingest_stack(j.rast_fns, j.grid_xy, j.mask_fns, bands=[1, 2], pixels=spans)
+    assert sub['n_pix'] == P and sub['bands'].shape[-1] == 25 == sub['valid'].shape[-1]
+    assert [r[:2] for r in sub['ranges']] == spans
+    for p0, p1 in spans + [(P // 2 + 3, P // 2 + 9)]:
+        b, v = ingest.stack_range(sub, p0, p1)
+        assert np.array_equal(b, st['bands'][:, :, p0:p1]) and np.array_equal(v, st['valid'][:, p0:p1])
+    with pytest.raises(KeyError):
+        ingest.stack_range(sub, 6, 9)  # straddles a range end
+    empty = ingest.ingest_stack(j.rast_fns, j.grid_xy, j.mask_fns, bands=[1, 2], pixels=[])
+    assert empty['bands'].shape[-1] == 0 and empty['dates'] == st['dates']
 
 
 def test_job_setup_errors(tmp_path):

@@ -1,0 +1,249 @@
+// valu_peak.hip — measured VALU issue peak of one MI355X SIMD.
+//
+// The analyze kernel is bound by vector-instruction issue, so its roofline needs the rate at which
+// one SIMD issues wave64 VALU instructions of the kernel's own classes, at its own occupancy. This
+// program measures it with no memory traffic in the timed loop: each wave runs ITERS iterations of
+// a straight-line stream of register-only instructions (inline asm, eight independent chains per
+// class so no instruction waits on its predecessor), and the launch time gives wave-instructions
+// per second per SIMD; an s_memtime bracket per wave gives shader cycles per instruction.
+//
+// Occupancy is pinned with dynamic LDS: one wave per workgroup, 160 KiB / (4 W) bytes each, so at
+// most W waves share a SIMD (4 W per CU). Kinds:
+//   add_u32, cndmask, cmp (32-bit VALU), fma_f32, add_f64, fma_f64, mul_f64, rcp_f64,
+//   lshl_b64 (64-bit integer), mix_c2 (the analyze kernel's c2 PMC mix, profiles/r0?_pmc_c2.json:
+//   21 % FP64, 1.5 % INT64, the rest 32-bit, plus half as many SALU instructions as VALU).
+// Output: one JSON object on stdout. Nothing here stores through the scalar cache: results leave
+// through ordinary vector global stores.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#define CHECK(x)                                                              \
+  do {                                                                        \
+    hipError_t e_ = (x);                                                      \
+    if (e_ != hipSuccess) {                                                   \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      exit(1);                                                                \
+    }                                                                         \
+  } while (0)
+
+enum Kind { ADD_U32, CNDMASK, CMP, FMA_F32, FMA_F32K, ADD_F64, FMA_F64, MUL_F64, RCP_F64, LSHL_B64,
+            MIX_C2, NKIND };
+static const char* kKindName[NKIND] = {"add_u32", "cndmask_b32", "cmp_gt_u32", "fma_f32",
+                                       "fma_f32_k", "add_f64", "fma_f64", "mul_f64", "rcp_f64",
+                                       "lshlrev_b64", "mix_c2"};
+// VALU / SALU instructions per loop iteration of each kind (the asm blocks below)
+static const int kValuPerIter[NKIND] = {64, 64, 64, 64, 64, 64, 64, 64, 32, 64, 103};
+static const int kSaluPerIter[NKIND] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 50};
+
+#define R8(s) s s s s s s s s
+
+template <int K>
+__global__ void __launch_bounds__(64) valu_kernel(unsigned* out, unsigned long long* cyc, int iters) {
+  extern __shared__ unsigned lds_pad[];  // occupancy only
+  const unsigned t = threadIdx.x + blockIdx.x * 64u;
+  unsigned a0 = t, a1 = t + 1, a2 = t + 2, a3 = t + 3, a4 = t + 4, a5 = t + 5, a6 = t + 6, a7 = t + 7;
+  const unsigned inc = (t & 3) + 1;
+  float f0 = a0, f1 = a1, f2 = a2, f3 = a3, f4 = a4, f5 = a5, f6 = a6, f7 = a7;
+  const float fm = 1.0000001f, fa = 0.5f;
+  double d0 = a0, d1 = a1, d2 = a2, d3 = a3, d4 = a4, d5 = a5, d6 = a6, d7 = a7;
+  const double dm = 1.0000000001, da = 0.25;
+  unsigned long long q0 = a0, q1 = a1, q2 = a2, q3 = a3, q4 = a4, q5 = a5, q6 = a6, q7 = a7;
+  unsigned long long m0 = 0, m1 = 0, m2 = 0, m3 = 0, m4 = 0, m5 = 0, m6 = 0, m7 = 0;
+  const unsigned long long sel = (blockIdx.x & 1) ? ~0ull : 0x5555555555555555ull;
+  unsigned s0 = 1, s1 = 2, s2 = 3, s3 = 4;
+  if (lds_pad[0] == 0xdeadbeefu && t == 0xffffffffu) a0 = 0;  // keeps the LDS allocation
+  unsigned long long c0;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(c0)::"memory");
+  for (int it = 0; it < iters; it++) {
+    if constexpr (K == ADD_U32) {
+      asm volatile(R8("v_add_u32 %0, %0, %8\n v_add_u32 %1, %1, %8\n v_add_u32 %2, %2, %8\n v_add_u32 %3, %3, %8\n"
+                      "v_add_u32 %4, %4, %8\n v_add_u32 %5, %5, %8\n v_add_u32 %6, %6, %8\n v_add_u32 %7, %7, %8\n")
+                   : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)
+                   : "v"(inc));
+    } else if constexpr (K == CNDMASK) {
+      asm volatile(R8("v_cndmask_b32_e64 %0, %0, %8, %9\n v_cndmask_b32_e64 %1, %1, %8, %9\n"
+                      "v_cndmask_b32_e64 %2, %2, %8, %9\n v_cndmask_b32_e64 %3, %3, %8, %9\n"
+                      "v_cndmask_b32_e64 %4, %4, %8, %9\n v_cndmask_b32_e64 %5, %5, %8, %9\n"
+                      "v_cndmask_b32_e64 %6, %6, %8, %9\n v_cndmask_b32_e64 %7, %7, %8, %9\n")
+                   : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)
+                   : "v"(inc), "s"(sel));
+    } else if constexpr (K == CMP) {
+      asm volatile(R8("v_cmp_gt_u32_e64 %0, %8, %9\n v_cmp_gt_u32_e64 %1, %8, %10\n"
+                      "v_cmp_gt_u32_e64 %2, %8, %11\n v_cmp_gt_u32_e64 %3, %8, %12\n"
+                      "v_cmp_gt_u32_e64 %4, %8, %13\n v_cmp_gt_u32_e64 %5, %8, %14\n"
+                      "v_cmp_gt_u32_e64 %6, %8, %15\n v_cmp_gt_u32_e64 %7, %8, %9\n")
+                   : "=s"(m0), "=s"(m1), "=s"(m2), "=s"(m3), "=s"(m4), "=s"(m5), "=s"(m6), "=s"(m7)
+                   : "v"(inc), "v"(a0), "v"(a1), "v"(a2), "v"(a3), "v"(a4), "v"(a5), "v"(a6));
+      a7 += (unsigned)(m0 ^ m1 ^ m2 ^ m3 ^ m4 ^ m5 ^ m6 ^ m7);
+    } else if constexpr (K == FMA_F32) {
+      asm volatile(R8("v_fma_f32 %0, %0, %8, %9\n v_fma_f32 %1, %1, %8, %9\n v_fma_f32 %2, %2, %8, %9\n"
+                      "v_fma_f32 %3, %3, %8, %9\n v_fma_f32 %4, %4, %8, %9\n v_fma_f32 %5, %5, %8, %9\n"
+                      "v_fma_f32 %6, %6, %8, %9\n v_fma_f32 %7, %7, %8, %9\n")
+                   : "+v"(f0), "+v"(f1), "+v"(f2), "+v"(f3), "+v"(f4), "+v"(f5), "+v"(f6), "+v"(f7)
+                   : "v"(fm), "v"(fa));
+    } else if constexpr (K == FMA_F32K) {  // two VGPR sources and an inline constant
+      asm volatile(R8("v_fma_f32 %0, %0, %8, 0.5\n v_fma_f32 %1, %1, %8, 0.5\n v_fma_f32 %2, %2, %8, 0.5\n"
+                      "v_fma_f32 %3, %3, %8, 0.5\n v_fma_f32 %4, %4, %8, 0.5\n v_fma_f32 %5, %5, %8, 0.5\n"
+                      "v_fma_f32 %6, %6, %8, 0.5\n v_fma_f32 %7, %7, %8, 0.5\n")
+                   : "+v"(f0), "+v"(f1), "+v"(f2), "+v"(f3), "+v"(f4), "+v"(f5), "+v"(f6), "+v"(f7)
+                   : "v"(fm));
+    } else if constexpr (K == ADD_F64) {
+      asm volatile(R8("v_add_f64 %0, %0, %8\n v_add_f64 %1, %1, %8\n v_add_f64 %2, %2, %8\n"
+                      "v_add_f64 %3, %3, %8\n v_add_f64 %4, %4, %8\n v_add_f64 %5, %5, %8\n"
+                      "v_add_f64 %6, %6, %8\n v_add_f64 %7, %7, %8\n")
+                   : "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3), "+v"(d4), "+v"(d5), "+v"(d6), "+v"(d7)
+                   : "v"(da));
+    } else if constexpr (K == FMA_F64) {
+      asm volatile(R8("v_fma_f64 %0, %0, %8, %9\n v_fma_f64 %1, %1, %8, %9\n v_fma_f64 %2, %2, %8, %9\n"
+                      "v_fma_f64 %3, %3, %8, %9\n v_fma_f64 %4, %4, %8, %9\n v_fma_f64 %5, %5, %8, %9\n"
+                      "v_fma_f64 %6, %6, %8, %9\n v_fma_f64 %7, %7, %8, %9\n")
+                   : "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3), "+v"(d4), "+v"(d5), "+v"(d6), "+v"(d7)
+                   : "v"(dm), "v"(da));
+    } else if constexpr (K == MUL_F64) {
+      asm volatile(R8("v_mul_f64 %0, %0, %8\n v_mul_f64 %1, %1, %8\n v_mul_f64 %2, %2, %8\n"
+                      "v_mul_f64 %3, %3, %8\n v_mul_f64 %4, %4, %8\n v_mul_f64 %5, %5, %8\n"
+                      "v_mul_f64 %6, %6, %8\n v_mul_f64 %7, %7, %8\n")
+                   : "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3), "+v"(d4), "+v"(d5), "+v"(d6), "+v"(d7)
+                   : "v"(dm));
+    } else if constexpr (K == RCP_F64) {
+      asm volatile("v_rcp_f64 %0, %0\n v_rcp_f64 %1, %1\n v_rcp_f64 %2, %2\n v_rcp_f64 %3, %3\n"
+                   "v_rcp_f64 %4, %4\n v_rcp_f64 %5, %5\n v_rcp_f64 %6, %6\n v_rcp_f64 %7, %7\n"
+                   "v_rcp_f64 %0, %0\n v_rcp_f64 %1, %1\n v_rcp_f64 %2, %2\n v_rcp_f64 %3, %3\n"
+                   "v_rcp_f64 %4, %4\n v_rcp_f64 %5, %5\n v_rcp_f64 %6, %6\n v_rcp_f64 %7, %7\n"
+                   "v_rcp_f64 %0, %0\n v_rcp_f64 %1, %1\n v_rcp_f64 %2, %2\n v_rcp_f64 %3, %3\n"
+                   "v_rcp_f64 %4, %4\n v_rcp_f64 %5, %5\n v_rcp_f64 %6, %6\n v_rcp_f64 %7, %7\n"
+                   "v_rcp_f64 %0, %0\n v_rcp_f64 %1, %1\n v_rcp_f64 %2, %2\n v_rcp_f64 %3, %3\n"
+                   "v_rcp_f64 %4, %4\n v_rcp_f64 %5, %5\n v_rcp_f64 %6, %6\n v_rcp_f64 %7, %7\n"
+                   : "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3), "+v"(d4), "+v"(d5), "+v"(d6), "+v"(d7));
+    } else if constexpr (K == LSHL_B64) {
+      asm volatile(R8("v_lshlrev_b64 %0, 1, %0\n v_lshlrev_b64 %1, 1, %1\n v_lshlrev_b64 %2, 1, %2\n"
+                      "v_lshlrev_b64 %3, 1, %3\n v_lshlrev_b64 %4, 1, %4\n v_lshlrev_b64 %5, 1, %5\n"
+                      "v_lshlrev_b64 %6, 1, %6\n v_lshlrev_b64 %7, 1, %7\n")
+                   : "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3), "+v"(q4), "+v"(q5), "+v"(q6), "+v"(q7));
+    } else {  // MIX_C2: five blocks of the c2 analyze kernel's PMC mix
+#define MIXBLK(ADDF, LSH)                                                              \
+  asm volatile(ADDF                                                                    \
+               "v_fma_f64 %1, %1, %13, %14\n v_add_u32 %4, %4, %15\n"                  \
+               "v_cndmask_b32_e64 %5, %5, %15, %16\n v_cmp_gt_u32_e64 %8, %15, %4\n"   \
+               "v_add_u32 %6, %6, %15\n v_cndmask_b32_e64 %7, %7, %15, %16\n"          \
+               "s_add_u32 %9, %9, 1\n s_and_b32 %10, %10, %9\n"                        \
+               "v_bfe_u32 %5, %4, 3, 7\n v_mul_f64 %2, %2, %13\n"                      \
+               "v_cndmask_b32_e64 %4, %4, %15, %16\n v_add_u32 %7, %7, %15\n"          \
+               "s_add_u32 %11, %11, %9\n s_and_b32 %9, %9, %11\n"                      \
+               "v_cndmask_b32_e64 %6, %6, %15, %16\n v_cmp_gt_u32_e64 %8, %15, %5\n"   \
+               "v_add_f64 %3, %3, %14\n v_bfe_u32 %6, %7, 2, 9\n"                      \
+               "s_add_u32 %10, %10, %11\n s_and_b32 %11, %11, %10\n"                   \
+               "v_cndmask_b32_e64 %5, %5, %15, %16\n v_cndmask_b32_e64 %7, %7, %15, %16\n" \
+               "v_cmp_gt_u32_e64 %8, %15, %6\n v_fma_f64 %1, %1, %13, %14\n"           \
+               "s_add_u32 %9, %9, %10\n s_and_b32 %10, %10, %9\n"                      \
+               "v_bfe_u32 %4, %5, 1, 11\n v_cndmask_b32_e64 %6, %6, %15, %16\n"        \
+               LSH                                                                     \
+               "s_add_u32 %11, %11, 3\n s_and_b32 %9, %9, %11\n"                       \
+               : "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3), "+v"(a0), "+v"(a1), "+v"(a2), \
+                 "+v"(a3), "=s"(m0), "+s"(s0), "+s"(s1), "+s"(s2), "+v"(q0)            \
+               : "v"(dm), "v"(da), "v"(inc), "s"(sel)                                 \
+               : "scc")
+      // per block: fma_f64 x2, mul_f64 x1, add_f64 x1, add_u32 x3, cndmask x8, cmp x3, bfe x3
+      // = 20 VALU (+ one add_f64 in the first block, one lshlrev_b64 in two blocks), 10 SALU:
+      // 103 VALU, 21 FP64 (20.4 %), 2 INT64 (1.9 %), 50 SALU per iteration
+      MIXBLK("v_add_f64 %0, %0, %14\n", "");
+      MIXBLK("", "v_lshlrev_b64 %12, 1, %12\n");
+      MIXBLK("", "");
+      MIXBLK("", "v_lshlrev_b64 %12, 1, %12\n");
+      MIXBLK("", "");
+#undef MIXBLK
+    }
+  }
+  unsigned long long c1;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(c1)::"memory");
+  unsigned r = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7 ^ s0 ^ s1 ^ s2 ^ s3 ^ (unsigned)(m0 ^ q0 ^ q1 ^ q2 ^ q3 ^ q4 ^ q5 ^ q6 ^ q7);
+  r ^= (unsigned)(f0 + f1 + f2 + f3 + f4 + f5 + f6 + f7);
+  r ^= (unsigned)(long long)(d0 + d1 + d2 + d3 + d4 + d5 + d6 + d7);
+  out[t] = r;  // vector store
+  if (threadIdx.x == 0) cyc[blockIdx.x] = c1 - c0;  // vector store from lane 0
+}
+
+typedef void (*KFn)(unsigned*, unsigned long long*, int);
+static KFn kernel_of(int k) {
+  switch (k) {
+    case ADD_U32: return valu_kernel<ADD_U32>;
+    case CNDMASK: return valu_kernel<CNDMASK>;
+    case CMP: return valu_kernel<CMP>;
+    case FMA_F32: return valu_kernel<FMA_F32>;
+    case FMA_F32K: return valu_kernel<FMA_F32K>;
+    case ADD_F64: return valu_kernel<ADD_F64>;
+    case FMA_F64: return valu_kernel<FMA_F64>;
+    case MUL_F64: return valu_kernel<MUL_F64>;
+    case RCP_F64: return valu_kernel<RCP_F64>;
+    case LSHL_B64: return valu_kernel<LSHL_B64>;
+    default: return valu_kernel<MIX_C2>;
+  }
+}
+
+int main(int argc, char** argv) {
+  int iters = argc > 1 ? atoi(argv[1]) : 20000;
+  hipDeviceProp_t prop;
+  CHECK(hipGetDeviceProperties(&prop, 0));
+  const int cus = prop.multiProcessorCount;
+  const int simds = cus * 4;
+  const size_t lds_cu = 160 * 1024;
+  // one generation: every wave of the launch is resident from start to end, so the s_memtime
+  // bracket of each wave spans W co-resident waves per SIMD throughout
+  const int gens = 1;
+  const int wps[] = {1, 2, 4, 8};
+  const int max_waves = cus * 4 * 8 * gens;
+  unsigned* out;
+  unsigned long long* cyc;
+  CHECK(hipMalloc(&out, (size_t)max_waves * 64 * sizeof(unsigned)));
+  CHECK(hipMalloc(&cyc, (size_t)max_waves * sizeof(unsigned long long)));
+  std::vector<unsigned long long> hc(max_waves);
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  printf("{\"device\": \"%s\", \"gcn_arch\": \"%s\", \"cus\": %d, \"simds\": %d, \"clock_khz\": %d, "
+         "\"iters\": %d, \"generations\": %d, \"results\": [",
+         prop.name, prop.gcnArchName, cus, simds, prop.clockRate, iters, gens);
+  bool first = true;
+  for (int k = 0; k < NKIND; k++) {
+    KFn fn = kernel_of(k);
+    for (int w : wps) {
+      const size_t lds = lds_cu / (4 * w) - 256;  // <= 4 W one-wave workgroups per CU
+      CHECK(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      const int blocks = cus * 4 * w * gens;
+      hipLaunchKernelGGL(fn, dim3(blocks), dim3(64), lds, 0, out, cyc, iters / 8);  // warm
+      CHECK(hipGetLastError());
+      CHECK(hipEventRecord(e0));
+      hipLaunchKernelGGL(fn, dim3(blocks), dim3(64), lds, 0, out, cyc, iters);
+      CHECK(hipEventRecord(e1));
+      CHECK(hipEventSynchronize(e1));
+      float ms = 0;
+      CHECK(hipEventElapsedTime(&ms, e0, e1));
+      CHECK(hipMemcpy(hc.data(), cyc, blocks * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+      double cyc_sum = 0;
+      for (int b = 0; b < blocks; b++) cyc_sum += (double)hc[b];
+      const double cyc_wave = cyc_sum / blocks;
+      const double valu_wave = (double)kValuPerIter[k] * iters;
+      const double valu = valu_wave * blocks;
+      const double rate_simd = valu / (ms * 1e-3) / simds;  // wave-instructions / s / SIMD
+      // cycles per VALU instruction per SIMD while W waves share it (s_memtime = shader clock)
+      const double cpi_simd = cyc_wave / (valu_wave * w);
+      printf("%s{\"kind\": \"%s\", \"waves_per_simd\": %d, \"valu_per_wave\": %.0f, \"salu_per_wave\": %.0f, "
+             "\"ms\": %.4f, \"g_valu_per_s_chip\": %.2f, \"g_valu_per_s_simd\": %.5f, "
+             "\"wave_cycles\": %.0f, \"cycles_per_valu_simd\": %.4f, \"implied_clock_ghz\": %.4f}",
+             first ? "" : ", ", kKindName[k], w, valu_wave, (double)kSaluPerIter[k] * iters, ms,
+             valu / (ms * 1e-3) / 1e9, rate_simd / 1e9, cyc_wave, cpi_simd,
+             rate_simd * cpi_simd / 1e9);
+      first = false;
+      fflush(stdout);
+    }
+  }
+  printf("]}\n");
+  CHECK(hipFree(out));
+  CHECK(hipFree(cyc));
+  return 0;
+}
