@@ -57,7 +57,7 @@ def valu_peak():
             d = json.load(f)
         by = {(r['kind'], r['waves_per_simd']): r for r in d['results']}
         mix = by[('mix_c2', 4)]
-        det = {k: round(by[(k, 4)]['cycles_per_valu_simd'], 3)
+        det = {k: round(by[(k, 4)]['cycles_per_valu_simd_nominal'], 3)
                for k in ('add_u32', 'cndmask_b32', 'cmp_gt_u32', 'fma_f32', 'add_f64', 'fma_f64',
                          'mul_f64', 'rcp_f64', 'lshlrev_b64', 'mix_c2') if (k, 4) in by}
         return mix['g_valu_per_s_chip'], VALU_PEAK_FILE, det
@@ -333,6 +333,10 @@ def main():
                          'compared with every plane they wrote (0: skip; A/B timing runs only)')
     ap.add_argument('--serial-load', action='store_true',
                     help='run the index_eqn kernels on the analyze stream (no load stream)')
+    ap.add_argument('--index-eqn', default='B1 - B2',
+                    help='attribution runs: another index_eqn over the same two int16 bands, e.g. '
+                         '"(B1 - B2) * 2 / 2" (the same values through a program that is not a '
+                         'linear form: the JIT-fused load stage, lt_jit.h)')
     args = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -371,7 +375,7 @@ def main():
                           mask_format=os.environ.get('LT_MASK_FORMAT', 'bits'))
     params, rules = compile_params(cfg['line_cost'], cfg['rules'], cfg['mode'])
     eng = get_engine(local)
-    index_fn = eng.compile_index(IndexProgram('B1 - B2', band_dtype='int16'))
+    index_fn = eng.compile_index(IndexProgram(args.index_eqn, band_dtype='int16'))
     fields = ['status', 'matched', 'class_val', 'onset_year', 'duration', 'magnitude']
     if cfg['trendline']:
         fields += TRENDLINE_FIELDS
@@ -518,8 +522,10 @@ def main():
                    'obs': meta.n_obs, 'rules': len(rules), 'line_cost': cfg['line_cost'],
                    'tile_pixels': tile, 'tiles': len(mosaic.tiles), 'tiles_rank0': len(items),
                    'gather': bool(gather),
-                   'input': 'int16 bands B1, B2 + index_eqn "B1 - B2"' +
-                            (' (fused into the analyze kernel)' if runner.fused else ''),
+                   'input': 'int16 bands B1, B2 + index_eqn "%s"' % args.index_eqn +
+                            (' (fused into the analyze kernel%s)'
+                             % (': JIT kernels, lt_jit.h' if runner.jit is not None else '')
+                             if runner.fused else ''),
                    'parallelism': ('one mosaic, tiles round-robin over %d GPU(s), labels sent '
                                    'to rank 0' % world) if mosaic_cfg else
                                   ('one scene per GPU (%d), labels sent to rank 0' % world)},
@@ -559,10 +565,13 @@ def main():
         'exchange_check': xcheck,
         'load_stage': {
             'fused': runner.fused,
-            'kernel': ('analyze_fast_kernel (index_eqn "B1 - B2" as lt_index_lin, evaluated on '
-                       'each winner\'s band values; lt_index_kernel4 below only for comparison)'
+            'kernel': (('analyze_fast_kernel (index_eqn "%s" %s, evaluated on each winner\'s '
+                        'band values; lt_index_kernel4 below only for comparison)'
+                        % (args.index_eqn, 'inlined into the JIT kernels (lt_jit.h)'
+                           if runner.jit is not None else 'as lt_index_lin'))
                        if runner.fused else
-                       'lt_index_kernel4 (hiprtc, index_eqn "B1 - B2", int16 bands -> int16)'),
+                       'lt_index_kernel4 (hiprtc, index_eqn "%s", int16 bands -> int16)'
+                       % args.index_eqn),
             'ms_per_launch_overlapped': r(index_ms, 3),
             'alone': {'ms': round(index_alone_ms, 4), 'pixels': it0.tile.n,
                       'bytes': index_bytes,

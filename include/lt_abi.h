@@ -22,13 +22,15 @@
  */
 #ifndef LT_ABI_H
 #define LT_ABI_H
+#ifndef __HIPCC_RTC__  /* hiprtc (the JIT kernels) brings its own */
 #include <stdint.h>
+#endif
 
 #ifdef __cplusplus
 extern "C" {
 #endif
 
-#define LT_ABI_VERSION 5
+#define LT_ABI_VERSION 6
 #define LT_MAX_YEARS 64   /* distinct calendar years per scene (T <= 40 in every config) */
 #define LT_MAX_OBS 1024   /* observations per scene (K*T) */
 #define LT_MAX_RULES 16
@@ -112,6 +114,8 @@ typedef struct {
   int64_t coef[LT_LIN_MAX_BANDS]; /* coefficient of band plane s, modulo 2^64                */
 } lt_index_lin;
 
+typedef struct lt_index lt_index;  /* a compiled index_eqn program (lt_index_compile) */
+
 typedef struct {
   int64_t n_pix;              /* P                                                          */
   int64_t stride;             /* elements between obs planes (>= n_pix)                     */
@@ -136,6 +140,13 @@ typedef struct {
    * obs o is valid at pixel p (utils.py:353); used instead of obs_valid when set. The winner pick
    * then reads ceil(K/32) words per pixel instead of one byte per observation */
   const uint32_t* obs_valid_bits;
+  /* fused load stage for ANY index_eqn program (ABI 6): with obs_bands set and index a program
+   * from lt_index_compile, the value of obs o at pixel p is that program evaluated on the bands
+   * above and stored into its out_type, as lt_index_apply writes it; lin is ignored. The analyze
+   * and resolve kernels are then JIT-compiled (hiprtc) with the program inlined into the winner
+   * pick, once per program and kernel instance (cached in the context and on disk, lt_jit.h). The
+   * band planes have the program's band_type and n_bands; any band type, planar or interleaved */
+  const lt_index* index;
 } lt_tile_in;
 
 /* ---- load stage: settings.json index_eqn (utils.py:447-484 rast_algebra) -------------------- */
@@ -179,7 +190,6 @@ typedef struct {
   void* out;
   int64_t band_pix_stride;
 } lt_index_io;
-typedef struct lt_index lt_index;
 
 /* ---- settings.json compiled on the host (for non-Python hosts) -------------------------------- */
 /* The Python exception the reference raises for a rejected settings.json (lt_settings_compile). */

@@ -10,7 +10,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, 'liblt_hip.so')
 
-LT_ABI_VERSION = 5
+LT_ABI_VERSION = 6
 LT_MAX_YEARS = 64
 LT_MAX_OBS = 1024
 LT_MAX_RULES = 16
@@ -94,7 +94,8 @@ class LtTileIn(ctypes.Structure):
                 ('index_type', ctypes.c_int32), ('_pad', ctypes.c_int32),
                 ('obs_bands', ctypes.c_void_p), ('band_obs_stride', ctypes.c_int64),
                 ('band_stride', ctypes.c_int64), ('band_pix_stride', ctypes.c_int64),
-                ('lin', LtIndexLin), ('obs_valid_bits', ctypes.c_void_p)]
+                ('lin', LtIndexLin), ('obs_valid_bits', ctypes.c_void_p),
+                ('index', ctypes.c_void_p)]
 
 
 class LtIndexOp(ctypes.Structure):

@@ -16,6 +16,8 @@
 #include "lt_launch.h"
 #include "lt_pixel.h"
 #include "lt_index.h"
+#include "lt_jit.h"
+#include "lt_kernels_dev.h"
 #include "lt_settings.h"
 #include "lt_raster.h"
 
@@ -167,6 +169,9 @@ struct lt_ctx {
   bool set_used[2] = {false, false};
   int last_set = 0;
   std::map<std::string, lt_index*> index_fns;  // compiled load-stage kernels, by source
+  // JIT analyze / resolve kernels with an index_eqn program inlined (lt_jit.h), by program
+  // source and instance
+  std::map<std::string, lt_jit_kernels> jit;
 };
 
 static int fail(lt_ctx* c, int code, const char* fmt, const char* detail = "") {
@@ -254,6 +259,8 @@ int lt_ctx_destroy(lt_ctx* c) {
     if (c->ev_analyzed[s]) (void)hipEventDestroy(c->ev_analyzed[s]);
     if (c->ev_resolved[s]) (void)hipEventDestroy(c->ev_resolved[s]);
   }
+  for (auto& kv : c->jit)
+    if (kv.second.mod) (void)hipModuleUnload(kv.second.mod);
   if (c->d_defer) (void)hipFree(c->d_defer);
   if (c->d_yflags) (void)hipFree(c->d_yflags);
   if (c->d_ndefer) (void)hipFree(c->d_ndefer);
@@ -299,6 +306,15 @@ static int check_tile(lt_ctx* c, const lt_tile_in* in, const lt_tile_out* out) {
     return fail(c, LT_ERR_ARG, "bad n_pix/stride%s");
   if (in->n_pix > LT_MAX_TILE_PIX) return fail(c, LT_ERR_LIMIT, "tile above LT_MAX_TILE_PIX%s");
   if (in->n_pix == 0) return LT_OK;  // nothing is read or written
+  if (in->obs_bands && in->index) {  // the fused load stage, any program (JIT kernels)
+    const lt_index* f = in->index;
+    const bool planar = in->band_pix_stride == 1 && in->band_stride >= in->n_pix &&
+                        in->band_obs_stride >= (int64_t)f->n_bands * in->band_stride;
+    const bool interleaved = in->band_stride == 1 && in->band_pix_stride == f->n_bands &&
+                             in->band_obs_stride >= (int64_t)f->n_bands * in->n_pix;
+    if (!planar && !interleaved) return fail(c, LT_ERR_ARG, "bad band strides%s");
+    return LT_OK;
+  }
   if (in->obs_bands) {  // the fused load stage: a linear form lt_index_linearize accepts
     const lt_index_lin& L = in->lin;
     if (L.n_bands < 1 || L.n_bands > LT_LIN_MAX_BANDS ||
@@ -320,6 +336,30 @@ static int check_tile(lt_ctx* c, const lt_tile_in* in, const lt_tile_out* out) {
   if (!in->obs_val && !in->obs_index) return fail(c, LT_ERR_ARG, "obs_val or obs_index required%s");
   if (in->obs_index && !lt_idx::ctype(in->index_type))
     return fail(c, LT_ERR_ARG, "bad index_type%s");
+  return LT_OK;
+}
+
+// The JIT analyze / resolve kernels of program f for a tile of Y year slots and n_rules rules
+// (lt_jit.h): the instance the product would dispatch to (MAXY, RMAX buckets, series type),
+// compiled on first use and cached in the context.
+static int jit_kernels(lt_ctx* c, const lt_index* f, int Y, int n_rules,
+                       const lt_jit_kernels** out) {
+  const int maxy = Y <= 32 ? 32 : Y <= 48 ? 48 : 64;
+  const int rmax = n_rules <= 1 ? 1 : n_rules <= 4 ? 4 : 16;
+  const char* vt = lt_jit::series_type(f->out_type, n_rules);
+  std::string err;
+  const std::string src = lt_jit::source(f->prog, maxy, rmax, vt, err);
+  if (src.empty()) return fail(c, LT_ERR_ARG, "%s", err.c_str());
+  auto it = c->jit.find(src);
+  if (it == c->jit.end()) {
+    hipDeviceProp_t prop;
+    HIP_OR_FAIL(c, hipGetDeviceProperties(&prop, c->device));
+    lt_jit_kernels k;
+    if (!lt_jit::build(src, prop.gcnArchName, c->device, k, err))
+      return fail(c, LT_ERR_JIT, "%s", err.c_str());
+    it = c->jit.emplace(src, k).first;
+  }
+  *out = &it->second;
   return LT_OK;
 }
 
@@ -351,7 +391,24 @@ static int launch_tile(lt_ctx* c, const lt_params* prm, const lt_tile_in* in,
   const int64_t nwave = (in->n_pix + 63) / 64;
   if (nwave > 0x7fffffff) return fail(c, LT_ERR_LIMIT, "tile too large%s");
   lt::TileLaunch l{c->d_scene, prm, in, out, c->d_xtab, dl, dn, yf, Y, c->device, stream};
-  HIP_OR_FAIL(c, lt::launch_analyze(l));
+  const lt_jit_kernels* jk = nullptr;
+  if (in->obs_bands && in->index) {  // a program inlined into JIT kernels (lt_jit.h)
+    const int rc = jit_kernels(c, in->index, Y, prm->n_rules, &jk);
+    if (rc != LT_OK) return rc;
+  }
+  // the JIT kernels' one argument, as the product kernels get it (lt_kernels.h kernel_args)
+  auto jit_launch = [&](hipFunction_t f, unsigned grid, int64_t* list,
+                        unsigned long long* counters, hipStream_t s) -> hipError_t {
+    lt::KernelArgs a{c->d_scene, *prm, *in, *out, c->d_xtab, list, counters, yf};
+    size_t sz = sizeof a;
+    void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz,
+                   HIP_LAUNCH_PARAM_END};
+    return hipModuleLaunchKernel(f, grid, 1, 1, 64, 1, 1, 0, s, nullptr, cfg);
+  };
+  if (jk)
+    HIP_OR_FAIL(c, jit_launch(jk->analyze, (unsigned)nwave, dl, dn, stream));
+  else
+    HIP_OR_FAIL(c, lt::launch_analyze(l));
   if (ep[0]) HIP_OR_FAIL(c, hipEventRecord(ep[0]->stop, stream));
   if (rstream != stream) {
     HIP_OR_FAIL(c, hipEventRecord(c->ev_analyzed[set], stream));
@@ -360,7 +417,17 @@ static int launch_tile(lt_ctx* c, const lt_params* prm, const lt_tile_in* in,
   if (ep[1]) HIP_OR_FAIL(c, hipEventRecord(ep[1]->start, rstream));
   stream = rstream;  // the resolve launches below
   l.stream = rstream;
-  HIP_OR_FAIL(c, lt::launch_resolve(l));
+  if (jk) {  // the deferred lists, as launch_resolve_instance launches them
+    const unsigned g0 = jk->resolve_grid < (unsigned)nwave ? jk->resolve_grid : (unsigned)nwave;
+    HIP_OR_FAIL(c, jit_launch(jk->resolve, g0, dl, dn, stream));
+    if (jk->resolve64) {
+      const unsigned g1 =
+          jk->resolve64_grid < (unsigned)nwave ? jk->resolve64_grid : (unsigned)nwave;
+      HIP_OR_FAIL(c, jit_launch(jk->resolve64, g1, dl + in->n_pix, dn + 2, stream));
+    }
+  } else {
+    HIP_OR_FAIL(c, lt::launch_resolve(l));
+  }
   if (yf) {  // every pixel's flags are in (analyze + resolve): expand them into the planes
     const bool v4 = ((uintptr_t)out->spike % 4 == 0) && ((uintptr_t)out->vertex % 4 == 0) &&
                     out->stride % 4 == 0;
@@ -667,6 +734,7 @@ int lt_index_compile(lt_ctx* c, const lt_index_prog* prog, lt_index** out) {
   f->n_bands = prog->n_bands;
   f->band_type = prog->band_type;
   f->out_type = prog->out_type;
+  f->prog = *prog;
   if (hipModuleLoadData(&f->mod, code.data()) != hipSuccess ||
       hipModuleGetFunction(&f->fn, f->mod, "lt_index_kernel") != hipSuccess ||
       hipModuleGetFunction(&f->fn4, f->mod, "lt_index_kernel4") != hipSuccess ||

@@ -1,29 +1,27 @@
 // lt_dispatch.hip — the product's analyze / resolve instances (lt_kernels.h), chosen per tile by
 // the scene's year count (MAXY: the LDS series and DP arrays are sized for it) and the rule count
 // (RMAX: per-rule state in registers; up to LT_CERT_RULES rules take the certified labels path).
-#include "lt_kernels.h"
+// Each (MAXY, RMAX) pair is compiled in a translation unit of its own (lt_dispatch_unit.hip, built
+// once per pair with -DLT_UNIT_MAXY / -DLT_UNIT_RMAX), so the nine long compiles run side by side.
+#include "lt_dispatch_units.h"
 
 namespace lt {
 
 namespace {
-// waves per SIMD each instance is built for: 4 (<= 128 VGPRs) where the body fits without
-// spilling (5 for the c2 instance was measured slower: 1365 vs 2079 Mpx/s, spills)
-constexpr int kWaves = 4;
-
 template <int MAXY>
 hipError_t analyze_for(const TileLaunch& l) {
   const int r = l.params->n_rules;
-  if (r <= 1) return launch_analyze_instance<MAXY, 1, kWaves, NoProbe>(l);
-  if (r <= 4) return launch_analyze_instance<MAXY, 4, kWaves, NoProbe>(l);
-  return launch_analyze_instance<MAXY, 16, kWaves, NoProbe>(l);
+  if (r <= 1) return analyze_unit<MAXY, 1>(l);
+  if (r <= 4) return analyze_unit<MAXY, 4>(l);
+  return analyze_unit<MAXY, 16>(l);
 }
 
 template <int MAXY>
 hipError_t resolve_for(const TileLaunch& l) {
   const int r = l.params->n_rules;
-  if (r <= 1) return launch_resolve_instance<MAXY, 1>(l);
-  if (r <= 4) return launch_resolve_instance<MAXY, 4>(l);
-  return launch_resolve_instance<MAXY, 16>(l);
+  if (r <= 1) return resolve_unit<MAXY, 1>(l);
+  if (r <= 4) return resolve_unit<MAXY, 4>(l);
+  return resolve_unit<MAXY, 16>(l);
 }
 }  // namespace
 

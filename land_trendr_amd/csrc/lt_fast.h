@@ -13,7 +13,9 @@
 //   * scratch: the analyze stage's OPT values of the DP (OPTa, read at wave-uniform indices
 //     below the four-column register window) and a few spills live in per-lane private memory.
 #pragma once
+#ifndef __HIPCC_RTC__  // hiprtc (the JIT kernels, lt_jit.h) brings its own
 #include <type_traits>
+#endif
 
 #include "lt_pixel.h"
 
@@ -143,6 +145,10 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
   // ---- pick_winners (utils.py:491-521) over wave-uniform year slots ----
   int T = 0, y0 = 0;
   uint64_t pres = 0;  // year slots with a winner: present point t is the t-th set bit
+  // int16 series: the values are integers of int16 range, so despike's standard deviation is
+  // compared through the exact sums S = sum v, Q = sum v^2 (see the despike below)
+  constexpr bool kIntSeries = std::is_same<VT, int16_t>::value;
+  double Ssum = 0.0, Qsum = 0.0;
   bool f32_bad = false;
   bool intdata = true;  // every value an integer of int16 range (lt_pixel.h sse_exact_zero)
   bool infdata = false;  // some value infinite (a binary32 series): the emulated fits fail (rc < 0)
@@ -294,6 +300,21 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
     using Uni = std::true_type;
     using Lane = std::false_type;
     const bool uni = !masked;  // launch-uniform
+#ifdef LT_JIT_INDEX
+    // a JIT kernel (lt_jit.h): the tile's index_eqn program is inlined as lt_jit_index (the load
+    // kernel's straight-line code and store, lt_index.h codegen), evaluated on every winner's
+    // band values, all the batch's band loads issued first
+    {
+      const LT_JIT_BAND_T* bb = (const LT_JIT_BAND_T*)in.obs_bands;
+      const LT_JIT_BAND_T* at[WB];
+#pragma unroll
+      for (int u = 0; u < WB; u++)
+        at[u] = bb + (uni ? row_of(u, Uni{}) : row_of(u, Lane{})) * in.band_obs_stride +
+                (int64_t)pp * in.band_pix_stride;
+#pragma unroll
+      for (int u = 0; u < WB; u++) val[u] = lt_jit_index(at[u], in.band_stride);
+    }
+#else
     if (in.obs_bands) {
       const lt_index_lin& LN = in.lin;
       const int wb = lin_type_bits(LN.wrap_type);
@@ -329,6 +350,7 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
       for (int u = 0; u < WB; u++)
         val[u] = obs_value(in, (int64_t)(best[u] >= 0 ? best[u] : 0), live ? p : 0);
     }
+#endif  // LT_JIT_INDEX
 #pragma unroll
     for (int u = 0; u < WB; u++) {
       const int y = yb + u;
@@ -340,7 +362,8 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
         const double v = val[u];
         if (T == 0) y0 = S.year[y];
         const VT vs = (VT)v;
-        if constexpr (!EXACT || sizeof(VT) < 8) {
+        // (an int16 series holds int16 index values, stored or evaluated: always exact)
+        if constexpr ((!EXACT || sizeof(VT) < 8) && !kIntSeries) {
           if (!((double)vs == v)) f32_bad = true;
         }
         if constexpr (!std::is_same<VT, int16_t>::value) {
@@ -348,6 +371,13 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
           if (__builtin_isinf(v)) infdata = true;
         }
         L.ys[T][lane] = vs;
+        if constexpr (kIntSeries) {
+          // the point's year offset (the scan below compacts it with its value) and the exact
+          // sums: integers below 2^53
+          L.xn[T][lane] = (uint8_t)(S.year[y] - y0);
+          Ssum += v;
+          Qsum = __builtin_fma(v, v, Qsum);
+        }
         pres |= 1ull << y;
         T++;
         if (out.val_raw) __builtin_nontemporal_store(v, out.val_raw + q);
@@ -367,7 +397,92 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
   // ---- despike (utils.py:556-582): numpy pairwise std, then the 3-window scan ----
   uint64_t spike = 0;
   int n = 0;
-  if (Tmax >= 2) {
+  if (kIntSeries && Tmax >= 2) {
+    // int16 series. The reference's sd is numpy's (pairwise sums of v and of (avg - v)^2, below
+    // in the general path); its only use is the test |y - x| > sd on an integer |y - x| <= 2^16.
+    // In exact arithmetic sd^2 = N / T^2 with N = T Q - S^2 (an integer < 2^43, exact here), so
+    // |d| > sd_exact <=> d^2 T^2 > N <=> |d| >= K, K = the least integer a with a^2 T^2 > N.
+    // numpy's sd is within 11.5 ulp (2^-49.5, relative) of sd_exact (pairwise sums of <= 64
+    // positive terms: <= 17 roundings on any term's path; avg's rounding only adds T (avg -
+    // S/T)^2 <= 2^-70 N/T), while an integer a <= 2^16 that is not sd_exact lies at least
+    // 1 / (2 a T^2) >= 2^-45 a from it (a^2 T^2 - N is a nonzero integer): the two tests agree
+    // for every |d| except |d| = sd_exact, an integer. Such a lane (N = a^2 T^2) takes numpy's
+    // sd (the pairwise sums, ballot-gated) to decide whether |d| = a counts as above it.
+    const double Td = (double)T, T2 = Td * Td;
+    const double N = __builtin_fma(Td, Qsum, -(Ssum * Ssum));
+    double a = ok ? __builtin_floor((double)__builtin_sqrtf((float)N) / Td) : 0.0;  // +-1
+    if (a * a * T2 > N) a -= 1.0;
+    if ((a + 1.0) * (a + 1.0) * T2 <= N) a += 1.0;
+    int K = (int)a + 1;  // |d| > sd <=> |d| >= K
+    const bool tie = ok && a * a * T2 == N;
+    if (__ballot(tie)) {
+      // numpy's sd for the lanes whose exact sd is the integer a: sequential-over-blocks
+      // pairwise sums as the general path computes them (np.sum)
+      const int n8 = (tie && T >= 8) ? T - (T % 8) : 0;
+      auto npsum = [&](auto term) {
+        double r[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+        for (int t0 = 0; t0 < n8; t0 += 8)
+          for (int u = 0; u < 8; u++) r[u] = t0 == 0 ? term(u) : r[u] + term(t0 + u);
+        double seq = n8 > 0 ? ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]))
+                            : 0.0;
+        for (int t = n8; t < T; t++) seq += term(t);
+        return seq;
+      };
+      if (tie) {
+        const double avg = npsum([&](int t) { return (double)L.ys[t][lane]; }) / Td;
+        const double sd = __builtin_sqrt(npsum([&](int t) {
+                                           const double d = avg - (double)L.ys[t][lane];
+                                           return d * d;
+                                         }) /
+                                         Td);
+        if (a > sd) K = (int)a;
+      }
+    }
+    // the 3-window scan in int32 (the values are exact), fused with dropna's compaction of the
+    // values and of the year offsets the winner pick stored (slot n <= t is written once point
+    // t's decision is known; this block's reads come first)
+    int last_good = ok ? (int)L.ys[0][lane] : 0;
+    int xv = last_good, yv = ok ? (int)L.ys[1][lane] : 0;
+    if (ok) n = 1;  // point 0 is never a spike (its offset, 0, is in place)
+    for (int t0 = 1; t0 < Tmax; t0 += 8) {
+      int z[8], xo[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        z[u] = t0 + u + 1 < Tmax ? (int)L.ys[t0 + u + 1][lane] : 0;
+        xo[u] = t0 + u < Tmax ? (int)L.xn[t0 + u][lane] : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const int t = t0 + u;
+        if (t >= Tmax) break;  // wave-uniform
+        if (!(ok && t < T)) continue;
+        const int cur = yv;
+        bool is_spike = false;
+        if (t + 1 < T) {  // the last point is never a spike
+          const int zv = z[u];
+          const int d1 = yv - xv, d2 = zv - yv;
+          // monotone <=> sign(d1) * sign(d2) >= 0
+          const int s1 = d1 < -1 ? -1 : (d1 > 1 ? 1 : d1), s2 = d2 < -1 ? -1 : (d2 > 1 ? 1 : d2);
+          const bool mono = __mul24(s1, s2) >= 0;
+          const int ad = __builtin_abs(d1) < __builtin_abs(d2) ? __builtin_abs(d1)
+                                                                : __builtin_abs(d2);
+          is_spike = !mono && ad >= K && yv != last_good;
+          if (!is_spike) last_good = yv;
+          xv = yv;
+          yv = zv;
+        }
+        if (is_spike) {
+          spike |= 1ull << t;
+          continue;
+        }
+        if (n != t) {
+          L.ys[n][lane] = (VT)cur;
+          L.xn[n][lane] = (uint8_t)xo[u];
+        }
+        n++;
+      }
+    }
+  } else if (Tmax >= 2) {
     // np.sum: n >= 8: eight accumulators over the first n - n%8 elements
     // (r_k starts as element k), their tree, then the rest sequentially; n < 8: sequential.
     // Two uniform loops: the accumulator block up to the wave's largest n8, the sequential tail

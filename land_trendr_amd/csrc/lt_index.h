@@ -18,6 +18,7 @@ struct lt_index {
   hipModule_t mod = nullptr;
   hipFunction_t fn = nullptr, fn4 = nullptr, fn4i = nullptr;
   int32_t n_bands = 0, band_type = 0, out_type = 0;
+  lt_index_prog prog{};  // the program (JIT analyze kernels inline it, lt_jit.h)
 };
 
 namespace lt_idx {

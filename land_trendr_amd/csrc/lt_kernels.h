@@ -1,6 +1,6 @@
-// lt_kernels.h — the analyze and resolve kernels around the wave-lockstep body of lt_fast.h, and
-// the launch of one (MAXY, RMAX) instance pair. Included by the dispatch translation units only
-// (lt_dispatch.hip: every instance the product needs; the profiling units of profiles/: one
+// lt_kernels.h — the analyze and resolve kernels (bodies in lt_kernels_dev.h) and the launch of
+// one (MAXY, RMAX) instance pair. Included by the dispatch translation units only
+// (lt_dispatch_unit.hip: every instance the product needs; the profiling units of profiles/: one
 // instance with a phase probe).
 //
 // Replaces, per pixel tile, the per-grid-point loop of MRLandTrendrJob.analysis_reducer
@@ -9,90 +9,25 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "lt_fast.h"
+#include "lt_kernels_dev.h"
 #include "lt_launch.h"
 
 namespace lt {
 
-__device__ inline void defer_append(bool deferred, int64_t p, int lane, int64_t* __restrict__ list,
-                                    unsigned long long* __restrict__ count) {
-  const uint64_t mask = __ballot(deferred);
-  if (mask == 0) return;
-  const int leader = __ffsll((long long)mask) - 1;
-  unsigned long long base = 0;
-  if (lane == leader) base = atomicAdd(count, (unsigned long long)__popcll(mask));
-  base = __shfl(base, leader);
-  if (deferred) list[base + __popcll(mask & ((1ull << lane) - 1))] = p;
-}
-
-// Every argument of the analyze / resolve kernels, passed as ONE by-value struct. The kernels read
-// its fields through the kernarg segment pointer at their uses (args()), so a field is loaded
-// where a stage needs it: a kernel that names its by-value parameters gets every one of them
-// loaded into SGPRs at entry (AMDGPU lowers kernel arguments there), and the ~60 SGPRs of tile
-// pointers and rule fields then live through the DP as SGPR spills in VGPR lanes (a lane VGPR
-// taken from the DP, a v_readlane per use).
-struct KernelArgs {
-  const DevScene* S;
-  lt_params P;
-  lt_tile_in in;
-  lt_tile_out out;
-  const lsq_xf* xtab;
-  int64_t* defer;
-  unsigned long long* n_defer;  // analyze: [0]/[2] list counts; resolve: its counters
-  uint64_t* yflags;
-};
-
-__device__ inline const KernelArgs& args() {
-  return *(const KernelArgs*)__builtin_amdgcn_kernarg_segment_ptr();
-}
-
-// Stage 1 (wave-lockstep body, lt_fast.h): one wave per workgroup, the pixel series in LDS.
-// WAVES: the waves per SIMD the instance is built for (<= 128 VGPRs at 4). VT: the LDS type of
-// the series — int16 when the tile's index raster is int16 (every value fits; half the LDS of
-// binary32, so more waves per CU), binary64 for binary64 values, else binary32 (values it cannot
-// hold defer the pixel to the binary64 resolve). Probe: lt_fast.h's phase probe (NoProbe here;
-// the profiling units of profiles/ pass theirs).
+// WAVES: the waves per SIMD the instance is built for (<= 128 VGPRs at 4)
 template <int MAXY, int RMAX, class VT, int WAVES, class Probe>
 __global__ __launch_bounds__(64, WAVES) void analyze_fast_kernel(const KernelArgs A) {
   (void)A;  // read through args()
-  __shared__ WaveLds<MAXY, VT, false> L;
-  const KernelArgs& K = args();
-  const int lane = threadIdx.x;
-  const int64_t p = (int64_t)blockIdx.x * 64 + lane;
-  const int64_t n_pix = K.in.n_pix;
-  const bool live = p < n_pix;
-  const int d = analyze_fast<MAXY, RMAX, false, VT>(*K.S, K.P, K.in, K.out, K.xtab, K.yflags, p,
-                                                    live, lane, L, Probe{});
-  // two lists: [0, n_pix) for the binary32 resolve, [n_pix, 2 n_pix) for the binary64 one;
-  // counters [0] / [2] count them (wave-aggregated atomics)
-  const KernelArgs& K2 = args();
-  defer_append(live && d == kDeferExact, p, lane, K2.defer, &K2.n_defer[0]);
-  defer_append(live && d == kDeferWide, p, lane, K2.defer + K2.in.n_pix, &K2.n_defer[2]);
+  analyze_body<MAXY, RMAX, VT, Probe>();
 }
 
-// Stage 2 (wave-lockstep, lt_fast.h with EXACT): the deferred pixels, binary64 series in LDS,
-// exact-OPT DP. A grid of exactly the resident waves takes 64-pixel groups of the list from a
-// counter (group cost varies a lot); every wave leaves once the counter has passed the list.
+// Built for 4 waves per SIMD like the analyze kernel (<= 128 VGPRs; the compiler's own choice
+// was 170, 2 waves): each resolve wave beside the next tile's analyze launch then holds the
+// registers of one analyze wave, not two (c2 21.62 vs 21.67 ms per step, profiles/r04_run3).
 template <int MAXY, int RMAX, class VT>
-__global__ __launch_bounds__(64) void resolve_fast_kernel(const KernelArgs A) {
+__global__ __launch_bounds__(64, 4) void resolve_fast_kernel(const KernelArgs A) {
   (void)A;  // read through args()
-  __shared__ WaveLds<MAXY, VT, true> L;
-  const int lane = threadIdx.x;
-  const KernelArgs& K = args();
-  unsigned long long* counters = K.n_defer;
-  const int64_t n = (int64_t)counters[0];  // written by stage 1, a previous launch
-  for (;;) {
-    unsigned g = 0;
-    if (lane == 0) g = atomicAdd((unsigned*)&counters[1], 1u);
-    g = __builtin_amdgcn_readfirstlane(__shfl(g, 0));
-    const int64_t base = (int64_t)g * 64;
-    if (base >= n) break;
-    const int64_t k = base + lane;
-    const bool live = k < n;
-    const KernelArgs& Kk = args();
-    analyze_fast<MAXY, RMAX, true, VT>(*Kk.S, Kk.P, Kk.in, Kk.out, Kk.xtab, Kk.yflags,
-                                       live ? Kk.defer[k] : 0, live, lane, L);
-  }
+  resolve_body<MAXY, RMAX, VT>();
 }
 
 // waves of resolve_fast_kernel<MAXY, RMAX, VT> the device holds at once

@@ -1,0 +1,94 @@
+// lt_kernels_dev.h — device side of the analyze / resolve kernels: their one by-value argument
+// struct and their bodies around the wave-lockstep analysis of lt_fast.h. Included by lt_kernels.h
+// (the product's __global__ instances and their launches) and by the JIT kernels of lt_jit.h
+// (hiprtc, an index_eqn program inlined into the winner pick), which therefore share the
+// argument layout and the code.
+//
+// Replaces, per pixel tile, the per-grid-point loop of MRLandTrendrJob.analysis_reducer
+// (/root/reference/mr_land_trendr_job.py:83-126) around utils.analyze + utils.change_labeling.
+#pragma once
+#include "lt_fast.h"
+
+namespace lt {
+
+__device__ inline void defer_append(bool deferred, int64_t p, int lane, int64_t* __restrict__ list,
+                                    unsigned long long* __restrict__ count) {
+  const uint64_t mask = __ballot(deferred);
+  if (mask == 0) return;
+  const int leader = __ffsll((long long)mask) - 1;
+  unsigned long long base = 0;
+  if (lane == leader) base = atomicAdd(count, (unsigned long long)__popcll(mask));
+  base = __shfl(base, leader);
+  if (deferred) list[base + __popcll(mask & ((1ull << lane) - 1))] = p;
+}
+
+// Every argument of the analyze / resolve kernels, passed as ONE by-value struct. The kernels read
+// its fields through the kernarg segment pointer at their uses (args()), so a field is loaded
+// where a stage needs it: a kernel that names its by-value parameters gets every one of them
+// loaded into SGPRs at entry (AMDGPU lowers kernel arguments there), and the ~60 SGPRs of tile
+// pointers and rule fields then live through the DP as SGPR spills in VGPR lanes (a lane VGPR
+// taken from the DP, a v_readlane per use).
+struct KernelArgs {
+  const DevScene* S;
+  lt_params P;
+  lt_tile_in in;
+  lt_tile_out out;
+  const lsq_xf* xtab;
+  int64_t* defer;
+  unsigned long long* n_defer;  // analyze: [0]/[2] list counts; resolve: its counters
+  uint64_t* yflags;
+};
+
+__device__ inline const KernelArgs& args() {
+  return *(const KernelArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+}
+
+// Stage 1 (wave-lockstep body, lt_fast.h): one wave per workgroup, the pixel series in LDS.
+// VT: the LDS type of the series — int16 when the tile's index raster is int16 (every value
+// fits; half the LDS of
+// binary32, so more waves per CU), binary64 for binary64 values, else binary32 (values it cannot
+// hold defer the pixel to the binary64 resolve). Probe: lt_fast.h's phase probe (NoProbe here;
+// the profiling units of profiles/ pass theirs).
+template <int MAXY, int RMAX, class VT, class Probe>
+__device__ inline void analyze_body() {
+  __shared__ WaveLds<MAXY, VT, false> L;
+  const KernelArgs& K = args();
+  const int lane = threadIdx.x;
+  const int64_t p = (int64_t)blockIdx.x * 64 + lane;
+  const int64_t n_pix = K.in.n_pix;
+  const bool live = p < n_pix;
+  const int d = analyze_fast<MAXY, RMAX, false, VT>(*K.S, K.P, K.in, K.out, K.xtab, K.yflags, p,
+                                                    live, lane, L, Probe{});
+  // two lists: [0, n_pix) for the binary32 resolve, [n_pix, 2 n_pix) for the binary64 one;
+  // counters [0] / [2] count them (wave-aggregated atomics)
+  const KernelArgs& K2 = args();
+  defer_append(live && d == kDeferExact, p, lane, K2.defer, &K2.n_defer[0]);
+  defer_append(live && d == kDeferWide, p, lane, K2.defer + K2.in.n_pix, &K2.n_defer[2]);
+}
+
+// Stage 2 (wave-lockstep, lt_fast.h with EXACT): the deferred pixels (list n_defer[0] of
+// `defer`), exact-OPT DP. A grid of exactly the resident waves takes 64-pixel groups of the list from a
+// counter (group cost varies a lot); every wave leaves once the counter has passed the list.
+// For an int16 series the list of values binary32 cannot hold ([n_pix, 2 n_pix)) is empty.
+template <int MAXY, int RMAX, class VT>
+__device__ inline void resolve_body() {
+  __shared__ WaveLds<MAXY, VT, true> L;
+  const int lane = threadIdx.x;
+  const KernelArgs& K = args();
+  unsigned long long* counters = K.n_defer;
+  const int64_t n = (int64_t)counters[0];  // written by stage 1, a previous launch
+  for (;;) {
+    unsigned g = 0;
+    if (lane == 0) g = atomicAdd((unsigned*)&counters[1], 1u);
+    g = __builtin_amdgcn_readfirstlane(__shfl(g, 0));
+    const int64_t base = (int64_t)g * 64;
+    if (base >= n) break;
+    const int64_t k = base + lane;
+    const bool live = k < n;
+    const KernelArgs& Kk = args();
+    analyze_fast<MAXY, RMAX, true, VT>(*Kk.S, Kk.P, Kk.in, Kk.out, Kk.xtab, Kk.yflags,
+                                       live ? Kk.defer[k] : 0, live, lane, L);
+  }
+}
+
+}  // namespace lt

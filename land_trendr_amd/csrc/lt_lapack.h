@@ -12,8 +12,10 @@
 // whole segment in ~20 registers. Functions are __host__ __device__ so the tests can run this exact
 // code on the CPU against the oracle (tests/native/lapack_host_check.hip).
 #pragma once
+#ifndef __HIPCC_RTC__  // hiprtc (the JIT kernels, lt_jit.h) brings its own
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#endif
 
 namespace lt {
 

@@ -9,8 +9,10 @@
 //   Trendline.parse_disturbances / match_rule (classes.py:156-232), change_labeling :795-820
 // All arithmetic that can decide a tie is the emulated LAPACK of lt_lapack.h.
 #pragma once
+#ifndef __HIPCC_RTC__  // hiprtc (the JIT kernels, lt_jit.h) brings its own
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#endif
 
 #include "../../include/lt_abi.h"
 #include "lt_lapack.h"

@@ -71,13 +71,15 @@ class Engine:
         return out
 
     def analyze_tile(self, scene, params, values, valid=None, fields=ALL_FIELDS, out=None,
-                     stream=None, lin=None):
+                     stream=None, lin=None, index=None):
         """values: [K, P] observation values — float64, or an index raster in its stored type
         (int16, uint16, int32, float32, uint8, ...: what index_tile writes) — valid: uint8 [K, P]
         or None. With lin (an IndexFn's linear form, fn.lin): values are the [K, NB, P] band
         planes and the kernel evaluates the index of each winner itself (the fused load stage).
+        With index (an IndexFn of any program): the same, with the program inlined into JIT
+        analyze / resolve kernels (lt_jit.h; compiled on first use, cached).
         Returns the dict of output tensors ([Y, P], [R, P], [P]); asynchronous on `stream`."""
-        tin, tout, out = self._tile_structs(scene, params, values, valid, fields, out, lin)
+        tin, tout, out = self._tile_structs(scene, params, values, valid, fields, out, lin, index)
         sc = scene.to_c()
         st = stream if stream is not None else torch.cuda.current_stream(self.device)
         rc = self.lib.lt_analyze_tile(self.ctx, ctypes.byref(sc), ctypes.byref(params),
@@ -87,12 +89,12 @@ class Engine:
         return out
 
     def analyze_tiles(self, scene, params, tiles, fields=ALL_FIELDS, outs=None, stream=None,
-                      ready=None, lin=None):
+                      ready=None, lin=None, index=None):
         """analyze_tile over a list of (values, valid) tiles of one scene in one call
         (lt_analyze_tiles: tile t's resolve stage overlaps tile t+1's analyze stage). ready: None
         or one recorded torch.cuda.Event (or None) per tile, which that tile's analyze kernel
         waits on (lt_analyze_tiles_after: the load stage of later tiles may still be running on
-        another stream). lin: as analyze_tile (every tile's values are then band planes).
+        another stream). lin / index: as analyze_tile (every tile's values are then band planes).
         Returns the list of output dicts; asynchronous on `stream`."""
         n = len(tiles)
         tins = (_abi.LtTileIn * max(n, 1))()
@@ -100,7 +102,7 @@ class Engine:
         res = []
         for t, (values, valid) in enumerate(tiles):
             tin, tout, o = self._tile_structs(scene, params, values, valid, fields,
-                                              outs[t] if outs is not None else None, lin)
+                                              outs[t] if outs is not None else None, lin, index)
             tins[t] = tin
             touts[t] = tout
             res.append(o)
@@ -120,16 +122,20 @@ class Engine:
         self._check(rc, 'lt_analyze_tiles')
         return res
 
-    def _tile_structs(self, scene, params, values, valid, fields, out, lin=None):
-        if lin is not None:  # the fused load stage: [K, NB, P] band planes
-            want = _TORCH_OF_LT.get(lin.band_type)
+    def _tile_structs(self, scene, params, values, valid, fields, out, lin=None, index=None):
+        if index is not None:  # any program, JIT kernels: its band type and band count
+            nb = len(index.program.bands)
+            want = _TORCH_OF_LT[_LT_T_OF_NP(index.program.band_dtype)]
+        elif lin is not None:
+            nb, want = lin.n_bands, _TORCH_OF_LT.get(lin.band_type)
+        if lin is not None or index is not None:  # the fused load stage: [K, NB, P] band planes
             planar = values.dim() == 3 and values.stride(2) == 1
-            inter = values.dim() == 3 and values.stride(1) == 1 and values.stride(2) == lin.n_bands
+            inter = values.dim() == 3 and values.stride(1) == 1 and values.stride(2) == nb
             if (values.dtype != want or values.device != self.device or values.dim() != 3 or
-                    values.shape[1] != lin.n_bands or not (planar or inter)):
+                    values.shape[1] != nb or not (planar or inter)):
                 raise LtError('bands must be a %s [K, %d, P] tensor on %s, planar (unit pixel '
                               'stride) or pixel-interleaved (unit band stride)'
-                              % (want, lin.n_bands, self.device))
+                              % (want, nb, self.device))
             K, _, P = values.shape
         else:
             if values.dtype not in _LT_T or values.device != self.device or values.dim() != 2:
@@ -145,10 +151,10 @@ class Engine:
                     valid.device != self.device):
                 raise LtError('valid bit planes must be an int32 [%d, P] tensor with unit pixel '
                               'stride' % W)
-            if lin is None and W > 1 and valid.stride(0) != values.stride(0):
+            if lin is None and index is None and W > 1 and valid.stride(0) != values.stride(0):
                 raise LtError('valid bit planes must share the row stride of values')
         elif valid is not None:
-            if lin is not None:
+            if lin is not None or index is not None:
                 if (valid.dtype != torch.uint8 or tuple(valid.shape) != (K, P) or
                         valid.stride(1) != 1 or valid.device != self.device):
                     raise LtError('valid must be a uint8 [K, P] tensor with unit pixel stride')
@@ -173,13 +179,16 @@ class Engine:
                     raise LtError('all [Y|R, P] outputs must share one row stride')
         tin = _abi.LtTileIn()
         tin.n_pix = P
-        if lin is not None:
+        if lin is not None or index is not None:
             tin.stride = valid.stride(0) if valid is not None and valid.shape[0] > 1 else P
             tin.obs_bands = values.data_ptr()
             tin.band_obs_stride = values.stride(0)
             tin.band_stride = values.stride(1)
             tin.band_pix_stride = values.stride(2)
-            tin.lin = lin
+            if index is not None:
+                tin.index = index.handle
+            else:
+                tin.lin = lin
         elif values.dtype == torch.float64:
             tin.stride = values.stride(0)
             tin.obs_val = ctypes.cast(values.data_ptr(), _abi.c_f64p)

@@ -2,11 +2,12 @@
 
 For every tile this rank owns (distributed.Mosaic), in tile order:
   1. load stage (parse_mapper's rast_algebra, mr_land_trendr_job.py:67-68 / utils.py:447-484):
-     when the index_eqn program is an integer linear form (engine.IndexFn.lin; 'B1 - B2' is one)
-     the analyze kernel evaluates it on the winners' band values itself (the fused load stage: no
-     index raster, no kernel between tiles); otherwise the hiprtc-compiled index_eqn kernel turns
-     the tile's band planes into its index raster, on a stream of its own, recording an event per
-     tile;
+     the analyze kernel evaluates the index_eqn program on the winners' band values itself (the
+     fused load stage: no index raster, no kernel between tiles) — an integer linear form
+     (engine.IndexFn.lin; 'B1 - B2' is one) in the precompiled kernel, any other program in JIT
+     kernels with the program inlined (lt_jit.h); with the fusion off (LT_FUSED_INDEX=0 /
+     LT_JIT_INDEX=0) the hiprtc-compiled index_eqn kernel turns the tile's band planes into its
+     index raster, on a stream of its own, recording an event per tile;
   2. analyze + label (analysis_reducer, mr_land_trendr_job.py:83-126): lt_analyze_tiles_after on
      the current stream, tile t waiting only for tile t's index event, so later tiles' load
      kernels (HBM-bound) run beside earlier tiles' analyze kernels (issue-bound); consecutive
@@ -89,17 +90,21 @@ class MosaicRunner:
         if self.ring:
             self.group = 1
         has_bands = any(it.bands is not None for it in self.items)
-        if has_bands and index_fn is None:
-            raise ValueError('band inputs need a compiled index_eqn (index_fn)')
         # (a CPU engine — the gloo tests' oracle double — has no streams: everything is serial)
         self.cuda = torch.device(engine.device).type == 'cuda'
-        # fused load stage (engine.IndexFn.lin): on unless fused=False or LT_FUSED_INDEX=0
+        if has_bands and index_fn is None:
+            raise ValueError('band inputs need a compiled index_eqn (index_fn)')
+        # fused load stage: on unless fused=False or LT_FUSED_INDEX=0. An integer linear program
+        # (engine.IndexFn.lin) runs in the precompiled analyze kernel; any other program in JIT
+        # analyze kernels with the program inlined (lt_jit.h; LT_JIT_INDEX=0 keeps the load
+        # kernel and its index raster for those)
         if fused is None:
             fused = os.environ.get('LT_FUSED_INDEX', '1') != '0'
-        self.lin = (getattr(index_fn, 'lin', None)
-                    if fused and has_bands and all(it.bands is not None for it in self.items)
-                    else None)
-        self.fused = self.lin is not None
+        all_bands = has_bands and all(it.bands is not None for it in self.items)
+        self.lin = getattr(index_fn, 'lin', None) if fused and all_bands else None
+        self.jit = (index_fn if fused and all_bands and self.lin is None and self.cuda and
+                    os.environ.get('LT_JIT_INDEX', '1') != '0' else None)
+        self.fused = self.lin is not None or self.jit is not None
         prio = int(os.environ.get('LT_LOAD_PRIORITY', '0'))
         self.load_stream = (torch.cuda.Stream(engine.device, priority=prio)
                             if self.cuda and has_bands and load_stream and not self.fused
@@ -202,7 +207,7 @@ class MosaicRunner:
             eng.analyze_tiles(
                 scene, self.params, tiles, self.fields,
                 outs=[{f: x[..., :nk] for f, x in self.outs[k].items()} for k, nk in zip(g, n)],
-                ready=ready, lin=self.lin)
+                ready=ready, lin=self.lin, index=self.jit)
             if stage_in is not None:
                 ev = torch.cuda.Event()
                 ev.record(main)

@@ -273,3 +273,85 @@ def test_fused_load_stage_one_pixel_planar_band_slice(engine):
     assert int(want['n_years'][0]) == 30
     for f in ALL_FIELDS:
         assert _bits_equal(want[f].cpu().numpy(), got[f].cpu().numpy()).all(), f
+
+
+JIT = [('(B1 - B2) * 1000 / (B1 + B2)', np.int16, None),   # NDVI-like: int16 floor division
+       ('(B1 - B2) * 2 / 2', np.int16, None),              # bench.py's attribution program
+       ('B1 / 2.0 - B2', np.int16, None),                  # a float64 node, stored into int16
+       ('B1 * B2 / 100', np.int16, np.float64),            # a product of bands, stored binary64
+       ('(B2 - B1) // 7 + B3', np.uint16, None)]           # unsigned floor division
+
+
+@pytest.mark.parametrize('eqn,bt,ot', JIT)
+@pytest.mark.parametrize('masked', [False, True])
+def test_jit_fused_load_stage_matches_index_raster_path(engine, eqn, bt, ot, masked):
+    """Programs that are not linear forms (divisions, float nodes, products of bands): the JIT
+    analyze / resolve kernels with the program inlined (lt_jit.h, lt_tile_in.index) write exactly
+    what the precompiled kernels write from the load kernel's index raster of the same bands, in
+    every output plane (x / 0 = 0 and wrapping values included)."""
+    from land_trendr_amd.engine import ALL_FIELDS
+    prog = index_eqn.IndexProgram(eqn, band_dtype=bt, out_dtype=ot)
+    fn = engine.compile_index(prog)
+    assert fn.lin is None
+    rng = np.random.default_rng(zlib.crc32((eqn + str(bt) + str(masked) + 'jit').encode()))
+    Y, P = 30, 6000
+    k_per = rng.integers(1, 4, Y) if masked else np.ones(Y, int)
+    dates = []
+    for y in range(Y):
+        for _ in range(k_per[y]):
+            dates.append('%d-%02d-%02d' % (1990 + y, rng.integers(5, 10), rng.integers(1, 28)))
+    K = len(dates)
+    meta = build_scene(dates, parse_date('2014-07-01'))
+    info = np.iinfo(np.dtype(bt))
+    lo, hi = max(int(info.min), -3000), min(int(info.max), 3000)
+    base = rng.integers(lo, hi + 1, (1, len(prog.bands), P))
+    b = np.clip(base + rng.integers(-400, 401, (K, len(prog.bands), P)), info.min, info.max)
+    b[:, :, :16] = rng.integers(info.min, int(info.max) + 1, (K, len(prog.bands), 16))  # extremes
+    b[:, :, 16:32] = 0  # zero denominators
+    bands = torch.from_numpy(b.astype(bt)).to(engine.device)
+    valid = None
+    if masked:
+        valid = torch.from_numpy((rng.random((K, P)) > 0.2).astype(np.uint8)).to(engine.device)
+    params, _ = compile_params(1.0, [{'name': 'gd', 'val': 1, 'change_type': 'GD'},
+                                     {'name': 'fd', 'val': 2, 'change_type': 'FD'}])
+    idx = engine.index_tile(fn, bands)
+    want = engine.analyze_tile(meta, params, idx, valid, ALL_FIELDS)
+    got = engine.analyze_tile(meta, params, bands, valid, ALL_FIELDS, index=fn)
+    torch.cuda.synchronize()
+    for f in ALL_FIELDS:
+        w, g = want[f].cpu().numpy(), got[f].cpu().numpy()
+        same = _bits_equal(w, g)
+        assert same.all(), '%s %s: %s differs in %d places' % (eqn, bt, f, (~same).sum())
+
+
+def test_jit_fused_runner_matches_oracle(engine):
+    """The mosaic runner with a non-linear program takes the JIT-fused path (runner.jit) and its
+    labels equal the oracle's on the index raster of the same bands."""
+    from land_trendr_amd.distributed import Mosaic
+    from land_trendr_amd.engine import valid_bytes
+    from land_trendr_amd.runner import MosaicRunner
+    from land_trendr_amd.synth import mosaic_inputs
+    from oracle import oracle
+    m = Mosaic([20000], 8192, 1, 0, 'by_scene')
+    items = mosaic_inputs(m, 30, 1, 3, 0.2, 91, engine.device, '2014-07-01')
+    params, _ = compile_params(10.0, [{'name': 'gd', 'val': 1, 'change_type': 'GD'}])
+    fn = engine.compile_index(index_eqn.IndexProgram('(B1 - B2) * 3 / 3', band_dtype=np.int16))
+    fields = ['status', 'matched', 'class_val', 'onset_year', 'duration', 'magnitude', 'val_fit',
+              'vertex']
+    r = MosaicRunner(engine, m, params, items, fields, fn)
+    assert r.fused and r.jit is fn and r.lin is None
+    r.step()
+    torch.cuda.synchronize()
+    for k, it in enumerate(r.items):
+        r.materialise_index(k)
+        vals = it.values.double().cpu().numpy()
+        want = oracle.analyze_tile(it.scene, params, vals,
+                                   valid_bytes(it.valid, it.scene.n_obs).cpu().numpy(),
+                                   n_threads=os.cpu_count() or 1)
+        for f in fields:
+            g = r.outs[k][f][..., :it.tile.n].cpu().numpy()
+            w = want[f][:g.shape[0]] if g.ndim == 2 else want[f]
+            if f in ('class_val', 'onset_year', 'duration', 'magnitude'):
+                mt = want['matched'].astype(bool)[:g.shape[0]]
+                g, w = np.where(mt, g, 0), np.where(mt, w, 0)
+            assert _bits_equal(w, g).all(), (k, f)

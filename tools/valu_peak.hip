@@ -32,13 +32,13 @@
   } while (0)
 
 enum Kind { ADD_U32, CNDMASK, CMP, FMA_F32, FMA_F32K, ADD_F64, FMA_F64, MUL_F64, RCP_F64, LSHL_B64,
-            MIX_C2, NKIND };
+            MIX_C2, MOV_B32, CNDMASK_VCC, NKIND };
 static const char* kKindName[NKIND] = {"add_u32", "cndmask_b32", "cmp_gt_u32", "fma_f32",
                                        "fma_f32_k", "add_f64", "fma_f64", "mul_f64", "rcp_f64",
-                                       "lshlrev_b64", "mix_c2"};
+                                       "lshlrev_b64", "mix_c2", "mov_b32", "cndmask_b32_vcc"};
 // VALU / SALU instructions per loop iteration of each kind (the asm blocks below)
-static const int kValuPerIter[NKIND] = {64, 64, 64, 64, 64, 64, 64, 64, 32, 64, 103};
-static const int kSaluPerIter[NKIND] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 50};
+static const int kValuPerIter[NKIND] = {64, 64, 64, 64, 64, 64, 64, 64, 32, 64, 103, 64, 64};
+static const int kSaluPerIter[NKIND] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 50, 0, 1};
 
 #define R8(s) s s s s s s s s
 
@@ -86,6 +86,19 @@ __global__ void __launch_bounds__(64) valu_kernel(unsigned* out, unsigned long l
                       "v_fma_f32 %6, %6, %8, %9\n v_fma_f32 %7, %7, %8, %9\n")
                    : "+v"(f0), "+v"(f1), "+v"(f2), "+v"(f3), "+v"(f4), "+v"(f5), "+v"(f6), "+v"(f7)
                    : "v"(fm), "v"(fa));
+    } else if constexpr (K == MOV_B32) {  // VOP1 moves (a rotation of eight registers)
+      asm volatile(R8("v_mov_b32 %0, %1\n v_mov_b32 %1, %2\n v_mov_b32 %2, %3\n v_mov_b32 %3, %4\n"
+                      "v_mov_b32 %4, %5\n v_mov_b32 %5, %6\n v_mov_b32 %6, %7\n v_mov_b32 %7, %0\n")
+                   : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7));
+    } else if constexpr (K == CNDMASK_VCC) {  // VOP2 selects on VCC (the e32 form)
+      asm volatile("s_mov_b64 vcc, %9\n"
+                   R8("v_cndmask_b32_e32 %0, %0, %8, vcc\n v_cndmask_b32_e32 %1, %1, %8, vcc\n"
+                      "v_cndmask_b32_e32 %2, %2, %8, vcc\n v_cndmask_b32_e32 %3, %3, %8, vcc\n"
+                      "v_cndmask_b32_e32 %4, %4, %8, vcc\n v_cndmask_b32_e32 %5, %5, %8, vcc\n"
+                      "v_cndmask_b32_e32 %6, %6, %8, vcc\n v_cndmask_b32_e32 %7, %7, %8, vcc\n")
+                   : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)
+                   : "v"(inc), "s"(sel)
+                   : "vcc");
     } else if constexpr (K == FMA_F32K) {  // two VGPR sources and an inline constant
       asm volatile(R8("v_fma_f32 %0, %0, %8, 0.5\n v_fma_f32 %1, %1, %8, 0.5\n v_fma_f32 %2, %2, %8, 0.5\n"
                       "v_fma_f32 %3, %3, %8, 0.5\n v_fma_f32 %4, %4, %8, 0.5\n v_fma_f32 %5, %5, %8, 0.5\n"
@@ -176,11 +189,14 @@ static KFn kernel_of(int k) {
     case CMP: return valu_kernel<CMP>;
     case FMA_F32: return valu_kernel<FMA_F32>;
     case FMA_F32K: return valu_kernel<FMA_F32K>;
+    case MOV_B32: return valu_kernel<MOV_B32>;
+    case CNDMASK_VCC: return valu_kernel<CNDMASK_VCC>;
     case ADD_F64: return valu_kernel<ADD_F64>;
     case FMA_F64: return valu_kernel<FMA_F64>;
     case MUL_F64: return valu_kernel<MUL_F64>;
     case RCP_F64: return valu_kernel<RCP_F64>;
     case LSHL_B64: return valu_kernel<LSHL_B64>;
+    case MIX_C2: return valu_kernel<MIX_C2>;
     default: return valu_kernel<MIX_C2>;
   }
 }
@@ -230,14 +246,16 @@ int main(int argc, char** argv) {
       const double valu_wave = (double)kValuPerIter[k] * iters;
       const double valu = valu_wave * blocks;
       const double rate_simd = valu / (ms * 1e-3) / simds;  // wave-instructions / s / SIMD
-      // cycles per VALU instruction per SIMD while W waves share it (s_memtime = shader clock)
-      const double cpi_simd = cyc_wave / (valu_wave * w);
+      // SIMD cycles per VALU instruction at the nominal clock (prop.clockRate), from the launch
+      // time. (The per-wave s_memtime span is reported as measured; it does not give cycles per
+      // instruction, as waves are not all co-resident from start to end: r04_run2 implied clocks
+      // of 0.8-2.4 GHz for one launch configuration.)
+      const double cpi_nominal = prop.clockRate * 1e3 / rate_simd;
       printf("%s{\"kind\": \"%s\", \"waves_per_simd\": %d, \"valu_per_wave\": %.0f, \"salu_per_wave\": %.0f, "
              "\"ms\": %.4f, \"g_valu_per_s_chip\": %.2f, \"g_valu_per_s_simd\": %.5f, "
-             "\"wave_cycles\": %.0f, \"cycles_per_valu_simd\": %.4f, \"implied_clock_ghz\": %.4f}",
+             "\"cycles_per_valu_simd_nominal\": %.4f, \"smemtime_cycles_per_wave\": %.0f}",
              first ? "" : ", ", kKindName[k], w, valu_wave, (double)kSaluPerIter[k] * iters, ms,
-             valu / (ms * 1e-3) / 1e9, rate_simd / 1e9, cyc_wave, cpi_simd,
-             rate_simd * cpi_simd / 1e9);
+             valu / (ms * 1e-3) / 1e9, rate_simd / 1e9, cpi_nominal, cyc_wave);
       first = false;
       fflush(stdout);
     }
