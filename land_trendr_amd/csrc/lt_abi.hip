@@ -342,13 +342,25 @@ static int check_tile(lt_ctx* c, const lt_tile_in* in, const lt_tile_out* out) {
 // The JIT analyze / resolve kernels of program f for a tile of Y year slots and n_rules rules
 // (lt_jit.h): the instance the product would dispatch to (MAXY, RMAX buckets, series type),
 // compiled on first use and cached in the context.
-static int jit_kernels(lt_ctx* c, const lt_index* f, int Y, int n_rules,
-                       const lt_jit_kernels** out) {
+static int jit_kernels(lt_ctx* c, const lt_index* f, int Y, const lt_params* prm,
+                       const lt_tile_in* in, const lt_tile_out* o, const lt_jit_kernels** out) {
+  const int n_rules = prm->n_rules;
   const int maxy = Y <= 32 ? 32 : Y <= 48 ? 48 : 64;
   const int rmax = n_rules <= 1 ? 1 : n_rules <= 4 ? 4 : 16;
   const char* vt = lt_jit::series_type(f->out_type, n_rules);
+  // specialised on the launch's uniform values too (lt_jit.h Spec) unless LT_JIT_SPEC=0
+  static const bool spec_on = !(getenv("LT_JIT_SPEC") && getenv("LT_JIT_SPEC")[0] == '0');
+  lt_jit::Spec sp;
+  if (spec_on) {
+    sp.on = true;
+    sp.n_years = Y;
+    sp.masked = in->obs_valid != nullptr || in->obs_valid_bits != nullptr;
+    sp.year_out = o->val_fit || o->fit_m || o->fit_b || o->right_m || o->right_b || o->spike ||
+                  o->vertex;
+    sp.params = *prm;
+  }
   std::string err;
-  const std::string src = lt_jit::source(f->prog, maxy, rmax, vt, err);
+  const std::string src = lt_jit::source(f->prog, maxy, rmax, vt, sp, err);
   if (src.empty()) return fail(c, LT_ERR_ARG, "%s", err.c_str());
   auto it = c->jit.find(src);
   if (it == c->jit.end()) {
@@ -393,7 +405,7 @@ static int launch_tile(lt_ctx* c, const lt_params* prm, const lt_tile_in* in,
   lt::TileLaunch l{c->d_scene, prm, in, out, c->d_xtab, dl, dn, yf, Y, c->device, stream};
   const lt_jit_kernels* jk = nullptr;
   if (in->obs_bands && in->index) {  // a program inlined into JIT kernels (lt_jit.h)
-    const int rc = jit_kernels(c, in->index, Y, prm->n_rules, &jk);
+    const int rc = jit_kernels(c, in->index, Y, prm, in, out, &jk);
     if (rc != LT_OK) return rc;
   }
   // the JIT kernels' one argument, as the product kernels get it (lt_kernels.h kernel_args)
@@ -405,10 +417,13 @@ static int launch_tile(lt_ctx* c, const lt_params* prm, const lt_tile_in* in,
                    HIP_LAUNCH_PARAM_END};
     return hipModuleLaunchKernel(f, grid, 1, 1, 64, 1, 1, 0, s, nullptr, cfg);
   };
+  // LT_SYNC_LAUNCH=1 (debugging): wait for each stage and report a fault against it
+  static const bool sync_each = getenv("LT_SYNC_LAUNCH") && getenv("LT_SYNC_LAUNCH")[0] == '1';
   if (jk)
     HIP_OR_FAIL(c, jit_launch(jk->analyze, (unsigned)nwave, dl, dn, stream));
   else
     HIP_OR_FAIL(c, lt::launch_analyze(l));
+  if (sync_each) HIP_OR_FAIL(c, hipStreamSynchronize(stream));
   if (ep[0]) HIP_OR_FAIL(c, hipEventRecord(ep[0]->stop, stream));
   if (rstream != stream) {
     HIP_OR_FAIL(c, hipEventRecord(c->ev_analyzed[set], stream));
@@ -420,14 +435,20 @@ static int launch_tile(lt_ctx* c, const lt_params* prm, const lt_tile_in* in,
   if (jk) {  // the deferred lists, as launch_resolve_instance launches them
     const unsigned g0 = jk->resolve_grid < (unsigned)nwave ? jk->resolve_grid : (unsigned)nwave;
     HIP_OR_FAIL(c, jit_launch(jk->resolve, g0, dl, dn, stream));
-    if (jk->resolve64) {
-      const unsigned g1 =
-          jk->resolve64_grid < (unsigned)nwave ? jk->resolve64_grid : (unsigned)nwave;
-      HIP_OR_FAIL(c, jit_launch(jk->resolve64, g1, dl + in->n_pix, dn + 2, stream));
+    // the second list (values binary32 cannot hold): empty for an int16 series (not launched,
+    // as launch_resolve_instance does), the binary64 resolve for a binary32 one, the same
+    // kernel for a binary64 one
+    const bool i16 = in->index->out_type == LT_T_I16;
+    if (!i16) {
+      hipFunction_t f64 = jk->resolve64 ? jk->resolve64 : jk->resolve;
+      const unsigned gw = jk->resolve64 ? jk->resolve64_grid : jk->resolve_grid;
+      const unsigned g1 = gw < (unsigned)nwave ? gw : (unsigned)nwave;
+      HIP_OR_FAIL(c, jit_launch(f64, g1, dl + in->n_pix, dn + 2, stream));
     }
   } else {
     HIP_OR_FAIL(c, lt::launch_resolve(l));
   }
+  if (sync_each) HIP_OR_FAIL(c, hipStreamSynchronize(stream));
   if (yf) {  // every pixel's flags are in (analyze + resolve): expand them into the planes
     const bool v4 = ((uintptr_t)out->spike % 4 == 0) && ((uintptr_t)out->vertex % 4 == 0) &&
                     out->stride % 4 == 0;

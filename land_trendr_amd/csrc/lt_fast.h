@@ -33,6 +33,25 @@
 #define LT_CERT_RULES 4
 #endif
 
+// Launch-uniform values a JIT kernel may be compiled for (lt_jit.h defines LT_SPEC_* for the
+// configuration it specialises; the precompiled kernels read them from the launch at run time):
+// the rules (LT_SPEC_NRULES rules lt_spec_rules[], pre_threshold mode), the line cost, the year
+// count, whether a cloud mask is given, whether any per-year plane is written
+#ifdef LT_SPEC_NRULES
+#define LT_NRULES LT_SPEC_NRULES
+#define LT_RULE(r) lt_spec_rules[r]
+#define LT_PRE_MODE LT_SPEC_PRE_MODE
+#else
+#define LT_NRULES P.n_rules
+#define LT_RULE(r) P.rules[r]
+#define LT_PRE_MODE P.pre_threshold_mode
+#endif
+#ifdef LT_SPEC_LINE_COST
+#define LT_LINE_COST LT_SPEC_LINE_COST
+#else
+#define LT_LINE_COST P.line_cost
+#endif
+
 namespace lt {
 
 // max over the 64 lanes of a wave (every lane must call it). readfirstlane makes the result an
@@ -134,7 +153,11 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
                                    uint64_t* __restrict__ yflags, int64_t p, bool live, int lane,
                                    WaveLds<MAXY, VT, EXACT>& L,
                                    const Probe& probe = Probe()) {
+#ifdef LT_SPEC_Y
+  constexpr int Y = LT_SPEC_Y;
+#else
   const int Y = S.n_years;
+#endif
   const int64_t is = in.stride, os = out.stride;
   const double nan = __builtin_nan("");
   int status = LT_ST_OK;
@@ -158,8 +181,13 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
   // the mask as bit planes (lt_tile_in.obs_valid_bits): up to 128 observations, the pixel's
   // words are loaded once, together, and the winner scan tests bits; a byte mask costs a load
   // per observation, each waited out before its year's comparison
+#ifdef LT_SPEC_MASKED
+  constexpr bool masked = LT_SPEC_MASKED != 0;
+  const bool vbits = masked && in.obs_valid_bits != nullptr && S.n_obs <= 128;
+#else
   const bool masked = in.obs_valid != nullptr || in.obs_valid_bits != nullptr;  // launch-uniform
   const bool vbits = in.obs_valid_bits != nullptr && S.n_obs <= 128;
+#endif
   uint32_t vw0 = 0, vw1 = 0, vw2 = 0, vw3 = 0;
   if (vbits) {
     const uint32_t* vb = in.obs_valid_bits;
@@ -592,7 +620,7 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
     if constexpr (MAXY <= LT_RESOLVE_PRIV_MAXY) {
       // ---- exact-OPT DP: closed-form intervals, then the emulated LAPACK residual for every
       // start whose interval reaches the column's smallest upper bound; first exact minimum ----
-      const double c = P.line_cost;
+      const double c = LT_LINE_COST;
       const double inf = __builtin_inf();
       // OPT lives in per-lane private memory (read at wave-uniform and per-lane indices)
       double OPT[MAXY + 1];
@@ -689,7 +717,7 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
     } else {  // larger series: OPT in registers (private memory would thrash L1)
       // ---- exact-OPT DP: closed-form intervals, then the emulated LAPACK residual for every
       // start whose interval reaches the column's smallest upper bound; first exact minimum ----
-      const double c = P.line_cost;
+      const double c = LT_LINE_COST;
       const double inf = __builtin_inf();
       double OPT[MAXY + 1];
 #pragma unroll
@@ -788,7 +816,7 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
       }
     }
   } else if (nmax >= 1) {
-    const double c = P.line_cost;
+    const double c = LT_LINE_COST;
     const double inf = __builtin_inf();
     double OPTa[MAXY + 1];  // per-lane private memory (wave-uniform indices)
     OPTa[0] = 0.0;
@@ -824,16 +852,18 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
       // interval enters the trackers at the end of the column)
       double Ve = inf, Hi = inf, L1 = inf, L2 = inf, v1 = inf, gv = inf;
       int ie = 0, i1 = 0, iL = -1, n1 = -1, gi = -1, gt = 0;
+      // (the bounds Hi, L1, L2 are only compared: v_min_f64 instead of a select pair; the values
+      // that become OPTa, v1 and Ve, are selected)
       auto track = [&](int i, double v, double hi, double lo, int nt) __attribute__((always_inline)) {
         if (hi <= Hi) {
           i1 = i;
           v1 = v;
           n1 = nt;
         }
-        Hi = hi <= Hi ? hi : Hi;
+        Hi = __builtin_fmin(hi, Hi);
         const bool bl = lo <= L1;
-        L2 = bl ? L1 : (lo < L2 ? lo : L2);
-        L1 = bl ? lo : L1;
+        L2 = bl ? L1 : __builtin_fmin(lo, L2);
+        L1 = __builtin_fmin(lo, L1);
         iL = bl ? i : iL;
       };
       // a zero-residual start (worth fl(c + OPTa[i]) in the reference) on OPTa[i] of tag tg
@@ -957,8 +987,7 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
       // start whose lower end lies above it can change no decision: it is neither the smallest
       // upper end nor among the lower ends at or below the final minimum bound H
       auto upper = [&]() __attribute__((always_inline)) {
-        const double h = Hi < Ve ? Hi : Ve;
-        return gh < h ? gh : h;
+        return __builtin_fmin(__builtin_fmin(Hi, Ve), gh);
       };
       // start i (>= 3 points, its point already in the sums): priced, offered to the trackers when
       // its lower end reaches the column's current upper bound (else it can change no decision),
@@ -1001,7 +1030,7 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
         const double w = __builtin_fma(0x1p-50, __builtin_fabs(gv), Emax);
         track(gi, gv, gv + w, gv - w, gt + 1);
       }
-      const double H = Hi < Ve ? Hi : Ve;  // the exact minimum lies in [min(L1, Ve), H]
+      const double H = __builtin_fmin(Hi, Ve);  // the exact minimum lies in [min(L1, Ve), H]
       int a, tnew;
       double vnew, enew = 0.0;
       if (L1 > H) {  // no inexact interval reaches H: the exact candidates decide
@@ -1020,14 +1049,14 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
         a = v1 <= Ve ? i1 : ie;
         vnew = v1 <= Ve ? v1 : Ve;
         tnew = (j + 1) << 8;
-        const double Lo = L1 < Ve ? L1 : Ve;
+        const double Lo = __builtin_fmin(L1, Ve);
         enew = (H - Lo) * (1.0 + 0x1p-40) + 0x1p-50 * __builtin_fabs(vnew);
       }
       if (col) {
         ag_set(j, a);
         OPTa[j + 1] = vnew;  // wave-uniform index
         if (tnew < 256) exact |= 2ull << j;
-        Emax = enew > Emax ? enew : Emax;
+        Emax = __builtin_fmax(enew, Emax);
         opt_jm3 = vnew;  // OPTa[j+1]: the slot of OPTa[j-3], which no later column reads
         tg_jm3 = tnew;
       }
@@ -1060,8 +1089,12 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
 
   // ---- vertices2eqns + eqns2fitted_points (utils.py:646-722) ----
   // per-year planes requested (launch-uniform)
+#ifdef LT_SPEC_YEAR_OUT
+  constexpr bool year_out = LT_SPEC_YEAR_OUT != 0;
+#else
   const bool year_out = out.val_fit || out.fit_m || out.fit_b || out.right_m || out.right_b ||
                         out.spike || out.vertex;
+#endif
   RuleState1 rs[RMAX];
   double prev_fit = 0.0;
   int32_t prev_year = 0;
@@ -1070,8 +1103,8 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
     if (q > 0) {
 #pragma unroll
       for (int r = 0; r < RMAX; r++)
-        if (r < P.n_rules)
-          rs[r].offer(P.rules[r], P.pre_threshold_mode, prev_year, yr - prev_year, prev_fit,
+        if (r < LT_NRULES)
+          rs[r].offer(LT_RULE(r), LT_PRE_MODE, prev_year, yr - prev_year, prev_fit,
                       prev_fit - fit_vertex, status);
     }
     prev_fit = fit_vertex;
@@ -1155,12 +1188,25 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
       }
       if (emit) {  // absent years and pixels the reference raises for: NaN / 0
         const int64_t o = (int64_t)y * os + p;
-        // write-once planes: nontemporal stores (same-box c5 A/B: 1012 vs 896-925 Mpx/s)
-        if (out.val_fit) __builtin_nontemporal_store(pr ? fv : nan, out.val_fit + o);
-        if (out.fit_m) __builtin_nontemporal_store(pr ? fmv : nan, out.fit_m + o);
-        if (out.fit_b) __builtin_nontemporal_store(pr ? fbv : nan, out.fit_b + o);
-        if (out.right_m) __builtin_nontemporal_store(pr ? cm : nan, out.right_m + o);
-        if (out.right_b) __builtin_nontemporal_store(pr ? cb : nan, out.right_b + o);
+        // write-once planes: nontemporal stores (same-box c5 A/B: 1012 vs 896-925 Mpx/s). When
+        // the year is present in every emitting lane (always, without a cloud mask) the values
+        // are stored as they are: no NaN select pair per plane
+        auto put = [&](double* plane, double v) __attribute__((always_inline)) {
+          if (plane) __builtin_nontemporal_store(v, plane + o);
+        };
+        if (__ballot(!pr) == 0) {
+          put(out.val_fit, fv);
+          put(out.fit_m, fmv);
+          put(out.fit_b, fbv);
+          put(out.right_m, cm);
+          put(out.right_b, cb);
+        } else {
+          put(out.val_fit, pr ? fv : nan);
+          put(out.fit_m, pr ? fmv : nan);
+          put(out.fit_b, pr ? fbv : nan);
+          put(out.right_m, pr ? cm : nan);
+          put(out.right_b, pr ? cb : nan);
+        }
         if (yflags) {
           spk |= (uint64_t)sp << y;
           vtx |= (uint64_t)isv << y;
@@ -1265,8 +1311,8 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
         const double wm = (wprev + w) + 0x1p-50 * (__builtin_fabs(fprev) + __builtin_fabs(fv));
 #pragma unroll
         for (int r = 0; r < RMAX; r++)
-          if (r < P.n_rules)
-            cand[r].offer(P.rules[r], P.pre_threshold_mode, yprev, yr - yprev, fprev - wprev,
+          if (r < LT_NRULES)
+            cand[r].offer(LT_RULE(r), LT_PRE_MODE, yprev, yr - yprev, fprev - wprev,
                           fprev + wprev, mag - wm, mag + wm, 1ull << ka, status);
       }
       am = cm;
@@ -1281,7 +1327,7 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
     uint64_t U = 0;
 #pragma unroll
     for (int r = 0; r < RMAX; r++)
-      if (r < P.n_rules) U |= cand[r].G;
+      if (r < LT_NRULES) U |= cand[r].G;
     if (infdata) U = vmask & (vmask - 1);
     const int nu = __builtin_popcountll(U);
     const int numax = wave_max(nu);
@@ -1327,8 +1373,8 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
       const int32_t du = (int32_t)L.xn[kq][lane] - (int32_t)L.xn[k1][lane];
 #pragma unroll
       for (int r = 0; r < RMAX; r++)
-        if (r < P.n_rules && act && (infdata || ((cand[r].G >> kq) & 1)))
-          rs[r].offer(P.rules[r], P.pre_threshold_mode, on, du, f1, f1 - fq, status);
+        if (r < LT_NRULES && act && (infdata || ((cand[r].G >> kq) & 1)))
+          rs[r].offer(LT_RULE(r), LT_PRE_MODE, on, du, f1, f1 - fq, status);
     }
   } else {
     // labels only, in lockstep over the vertex number q: the fitted value at each vertex is all
@@ -1381,7 +1427,7 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
   if (live && !deferred) {
 #pragma unroll
     for (int r = 0; r < RMAX; r++)
-      if (r < P.n_rules) rs[r].write(P.rules[r], out, (int64_t)r * os + p);
+      if (r < LT_NRULES) rs[r].write(LT_RULE(r), out, (int64_t)r * os + p);
   }
   probe.mark(4);
   if (!live || deferred) {

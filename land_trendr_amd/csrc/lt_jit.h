@@ -104,9 +104,28 @@ inline const char* series_type(int out_type, int n_rules) {
   return "float";
 }
 
-// The module source for program P, kernel instance (maxy, rmax) and series type vt; "" with err
+// The launch-uniform values a module is specialised for (lt_fast.h LT_SPEC_*): the scene's year
+// count, whether the tile has a cloud mask, whether any per-year plane is written, the rules, the
+// pre_threshold mode and the line cost. Constant-folded, they remove the code of every other case
+// (the mask scan, the year-major output loop or the labels-only paths, the rule filters).
+struct Spec {
+  bool on = false;
+  int n_years = 0;
+  bool masked = false, year_out = false;
+  lt_params params{};
+};
+
+inline std::string fmt_rule(const lt_rule& r) {
+  char b[256];
+  snprintf(b, sizeof b, "{%d, %d, %d, %d, %a, %a, %a, %d, 0}", r.change_type, r.onset_op,
+           r.duration_op, r.pre_op, r.onset_val, r.duration_val, r.pre_val, r.class_val);
+  return b;
+}
+
+// The module source for program P, kernel instance (maxy, rmax), series type vt and
+// specialisation sp; "" with err
 inline std::string source(const lt_index_prog& P, int maxy, int rmax, const char* vt,
-                          std::string& err) {
+                          const Spec& sp, std::string& err) {
   std::string store;
   const std::string body = lt_idx::codegen_body(P, false, err, store);
   if (body.empty()) return "";
@@ -116,6 +135,22 @@ inline std::string source(const lt_index_prog& P, int maxy, int rmax, const char
   src += lt_idx::kPrelude;
   snprintf(head, sizeof head, "#define LT_JIT_INDEX 1\n#define LT_JIT_BAND_T %s\n", BT);
   src += head;
+  if (sp.on) {
+    const lt_params& Q = sp.params;
+    char d[512];
+    snprintf(d, sizeof d,
+             "#include \"../../include/lt_abi.h\"\n#define LT_SPEC_Y %d\n#define LT_SPEC_MASKED %d\n"
+             "#define LT_SPEC_YEAR_OUT %d\n#define LT_SPEC_NRULES %d\n#define LT_SPEC_PRE_MODE %d\n"
+             "#define LT_SPEC_LINE_COST %a\n",
+             sp.n_years, sp.masked ? 1 : 0, sp.year_out ? 1 : 0, Q.n_rules, Q.pre_threshold_mode,
+             Q.line_cost);
+    src += d;
+    src += "__device__ constexpr lt_rule lt_spec_rules[" +
+           std::to_string(Q.n_rules > 0 ? Q.n_rules : 1) + "] = {";
+    for (int r = 0; r < (Q.n_rules > 0 ? Q.n_rules : 1); r++)
+      src += (r ? ", " : "") + fmt_rule(Q.rules[r]);
+    src += "};\n";
+  }
   src += "__device__ inline double lt_jit_index(const LT_JIT_BAND_T* b, long long band_stride) {\n";
   src += body;
   src += "  return (double)(" + store + ");\n}\n";
@@ -128,7 +163,9 @@ inline std::string source(const lt_index_prog& P, int maxy, int rmax, const char
            "lt::KernelArgs A) {\n  (void)A;\n  lt::resolve_body<%d, %d, %s>();\n}\n",
            maxy, rmax, vt, maxy, rmax, vt);
   src += k;
-  if (strcmp(vt, "short") != 0) {  // the values binary32 cannot hold: a binary64 resolve
+  // the values binary32 cannot hold: a binary64 resolve (a binary64 series uses lt_jit_resolve
+  // for both lists, as the product launches its one instance twice; an int16 series has none)
+  if (strcmp(vt, "float") == 0) {
     snprintf(k, sizeof k,
              "extern \"C\" __global__ __launch_bounds__(64, 4) void lt_jit_resolve64(const "
              "lt::KernelArgs A) {\n  (void)A;\n  lt::resolve_body<%d, %d, double>();\n}\n",
@@ -208,8 +245,15 @@ inline bool build(const std::string& src, const std::string& arch, int device,
     err = "JIT module load failed";
     return false;
   }
-  if (hipModuleGetFunction(&out.resolve64, out.mod, "lt_jit_resolve64") != hipSuccess)
-    out.resolve64 = nullptr;
+  // (a binary64 resolve exists for the non-int16 series types only: a failed lookup would leave
+  // "named symbol not found" as HIP's last error for the next launch check to find)
+  if (src.find("lt_jit_resolve64") != std::string::npos &&
+      hipModuleGetFunction(&out.resolve64, out.mod, "lt_jit_resolve64") != hipSuccess) {
+    (void)hipModuleUnload(out.mod);
+    out = lt_jit_kernels{};
+    err = "JIT module load failed (lt_jit_resolve64)";
+    return false;
+  }
   int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
       cus < 1)

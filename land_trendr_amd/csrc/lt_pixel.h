@@ -152,8 +152,8 @@ struct RuleCands {
       return;
     }
     G |= bit;
-    hi = khi > hi ? khi : hi;
-    if (!maybe) lo = klo > lo ? klo : lo;
+    hi = __builtin_fmax(khi, hi);  // (bounds: v_max_f64, not a select pair)
+    if (!maybe) lo = __builtin_fmax(klo, lo);
   }
 };
 

@@ -101,9 +101,14 @@ class MosaicRunner:
         if fused is None:
             fused = os.environ.get('LT_FUSED_INDEX', '1') != '0'
         all_bands = has_bands and all(it.bands is not None for it in self.items)
+        jit_ok = (fused and all_bands and self.cuda and
+                  os.environ.get('LT_JIT_INDEX', '1') != '0')
         self.lin = getattr(index_fn, 'lin', None) if fused and all_bands else None
-        self.jit = (index_fn if fused and all_bands and self.lin is None and self.cuda and
-                    os.environ.get('LT_JIT_INDEX', '1') != '0' else None)
+        # a linear program too goes to the JIT kernels, specialised for the job's configuration
+        # (lt_jit.h Spec), unless LT_JIT_LINEAR=0 keeps it on the precompiled kernels
+        if self.lin is not None and jit_ok and os.environ.get('LT_JIT_LINEAR', '1') != '0':
+            self.lin = None
+        self.jit = index_fn if jit_ok and self.lin is None else None
         self.fused = self.lin is not None or self.jit is not None
         prio = int(os.environ.get('LT_LOAD_PRIORITY', '0'))
         self.load_stream = (torch.cuda.Stream(engine.device, priority=prio)

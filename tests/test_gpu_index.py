@@ -208,7 +208,8 @@ FUSED = [('B1 - B2', np.int16, None), ('B1 * 300 - B2 * 300', np.int16, None),
          ('-(B1 - 2 * B3) + 30000', np.int16, None), ('B1 - B2', np.uint16, np.int16),
          ('(B2 - B1) * 2', np.uint16, None), ('B1 + B2 - 100', np.uint8, None),
          ('3 * B1 - B2', np.int32, None), ('B1 - B2', np.int16, np.float32),
-         ('B1 + 70000 - B2', np.int16, np.int16), ('B1 + 2 - B2 + B3 - B4', np.int16, None)]
+         ('B1 + 70000 - B2', np.int16, np.int16), ('B1 + 2 - B2 + B3 - B4', np.int16, None),
+         ('B1 - B2', np.int16, np.float64)]
 
 
 @pytest.mark.parametrize('eqn,bt,ot', FUSED)
