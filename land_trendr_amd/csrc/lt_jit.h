@@ -155,13 +155,16 @@ inline std::string source(const lt_index_prog& P, int maxy, int rmax, const char
   src += body;
   src += "  return (double)(" + store + ");\n}\n";
   src += "#include \"lt_kernels_dev.h\"\n";
+  // waves per SIMD the analyze kernel is built for (LT_JIT_WAVES, A/B runs; 4: <= 128 VGPRs)
+  const char* we = getenv("LT_JIT_WAVES");
+  const int waves = we && atoi(we) >= 1 && atoi(we) <= 8 ? atoi(we) : 4;
   char k[1024];
   snprintf(k, sizeof k,
-           "extern \"C\" __global__ __launch_bounds__(64, 4) void lt_jit_analyze(const "
+           "extern \"C\" __global__ __launch_bounds__(64, %d) void lt_jit_analyze(const "
            "lt::KernelArgs A) {\n  (void)A;\n  lt::analyze_body<%d, %d, %s, lt::NoProbe>();\n}\n"
            "extern \"C\" __global__ __launch_bounds__(64, 4) void lt_jit_resolve(const "
            "lt::KernelArgs A) {\n  (void)A;\n  lt::resolve_body<%d, %d, %s>();\n}\n",
-           maxy, rmax, vt, maxy, rmax, vt);
+           waves, maxy, rmax, vt, maxy, rmax, vt);
   src += k;
   // the values binary32 cannot hold: a binary64 resolve (a binary64 series uses lt_jit_resolve
   // for both lists, as the product launches its one instance twice; an int16 series has none)
