@@ -484,6 +484,11 @@ def main():
     meta = items[0].scene
     build = build_hash()
     pmc = pmc_summary(args.config, build)
+    # a summary taken on another kernel build describes other code: refused for the roofline
+    # (achieved / frac / traffic null), its figures kept beside it, marked as another build's
+    pmc_other = None
+    if pmc is not None and not pmc['_matches_build']:
+        pmc_other, pmc = pmc, None
     peak_g, peak_src, peak_cyc = valu_peak()
     valu_px = per_px(pmc, 'analyze', 'SQ_INSTS_VALU')
     achieved = (valu_px * px_per_launch / (kern_ms * 1e-3) / 1e9) if valu_px else None
@@ -541,9 +546,15 @@ def main():
                      'peak_source': peak_src, 'cycles_per_valu_at_4_waves': peak_cyc,
                      'build': build, 'pmc_build': pmc.get('_build') if pmc else None,
                      'pmc_matches_build': bool(pmc and pmc['_matches_build']),
+                     'pmc_refused': None if pmc_other is None else {
+                         'source': pmc_other['_path'], 'build': pmc_other.get('_build'),
+                         'reason': 'counters of another kernel build',
+                         'valu_instr_per_px': r(per_px(pmc_other, 'analyze', 'SQ_INSTS_VALU'), 2)},
                      'traffic': None if traffic_px is None else round(traffic_px * px_per_launch),
                      'traffic_source': pmc['_path'] if traffic_px is not None else None,
-                     'kernel': 'analyze_fast_kernel', 'kernel_ms': round(kern_ms, 3),
+                     'kernel': ('lt_jit_analyze (analyze_body JIT-compiled for this launch, '
+                                'lt_jit.h)' if runner.jit is not None else
+                                'analyze_fast_kernel'), 'kernel_ms': round(kern_ms, 3),
                      'valu_instr_per_px': r(valu_px, 2),
                      'pmc_valu_issue_frac': r(pmc_frac),  # the PMC launch alone (GRBM cycles at 2.4 GHz)
                      'step_valu_issue_frac': r(step_valu / peak_g if step_valu else None),
@@ -565,9 +576,10 @@ def main():
         'exchange_check': xcheck,
         'load_stage': {
             'fused': runner.fused,
-            'kernel': (('analyze_fast_kernel (index_eqn "%s" %s, evaluated on each winner\'s '
+            'kernel': (('%s (index_eqn "%s" %s, evaluated on each winner\'s '
                         'band values; lt_index_kernel4 below only for comparison)'
-                        % (args.index_eqn, 'inlined into the JIT kernels (lt_jit.h)'
+                        % ('lt_jit_analyze' if runner.jit is not None else 'analyze_fast_kernel',
+                           args.index_eqn, 'inlined into the JIT kernels (lt_jit.h)'
                            if runner.jit is not None else 'as lt_index_lin'))
                        if runner.fused else
                        'lt_index_kernel4 (hiprtc, index_eqn "%s", int16 bands -> int16)'

@@ -159,15 +159,19 @@ struct lt_ctx {
   size_t used = 0;               // pairs recorded since the last stage_ms call
   int64_t launches = 0;
   int64_t* d_defer = nullptr;    // deferred-pixel list of the resolve stage
-  uint64_t* d_yflags = nullptr;  // per-pixel spike / vertex year flags (2 sets x 2 planes)
+  uint64_t* d_yflags = nullptr;  // per-pixel spike / vertex year flags (kSets sets x 2 planes)
   unsigned long long* d_ndefer = nullptr;
   int64_t defer_cap = 0;
   lt::lsq_xf* d_xtab = nullptr;  // x-set factor table (built at context creation)
   hipStream_t side = nullptr;    // the resolve stage's stream (lt_analyze_tiles)
-  hipEvent_t ev_analyzed[2] = {nullptr, nullptr};  // per deferred-list set
-  hipEvent_t ev_resolved[2] = {nullptr, nullptr};
-  bool set_used[2] = {false, false};
-  int last_set = 0;
+  // deferred-list sets, used round robin by consecutive tiles (also across calls): tile t's
+  // set is reused by tile t + n_sets only after tile t's resolve
+  static constexpr int kSets = 3;
+  int n_sets = kSets;  // LT_DEFER_SETS (2..3) for A/B runs
+  hipEvent_t ev_analyzed[kSets] = {};
+  hipEvent_t ev_resolved[kSets] = {};
+  bool set_used[kSets] = {};
+  int last_set = 0, next_set = 0;
   std::map<std::string, lt_index*> index_fns;  // compiled load-stage kernels, by source
   // JIT analyze / resolve kernels with an index_eqn program inlined (lt_jit.h), by program
   // source and instance
@@ -255,7 +259,7 @@ int lt_ctx_destroy(lt_ctx* c) {
     (void)hipStreamSynchronize(c->side);
     (void)hipStreamDestroy(c->side);
   }
-  for (int s = 0; s < 2; s++) {
+  for (int s = 0; s < lt_ctx::kSets; s++) {
     if (c->ev_analyzed[s]) (void)hipEventDestroy(c->ev_analyzed[s]);
     if (c->ev_resolved[s]) (void)hipEventDestroy(c->ev_resolved[s]);
   }
@@ -343,7 +347,8 @@ static int check_tile(lt_ctx* c, const lt_tile_in* in, const lt_tile_out* out) {
 // (lt_jit.h): the instance the product would dispatch to (MAXY, RMAX buckets, series type),
 // compiled on first use and cached in the context.
 static int jit_kernels(lt_ctx* c, const lt_index* f, int Y, const lt_params* prm,
-                       const lt_tile_in* in, const lt_tile_out* o, const lt_jit_kernels** out) {
+                       const lt_tile_in* in, const lt_tile_out* o, const lt::DevScene* scene,
+                       const lt_jit_kernels** out) {
   const int n_rules = prm->n_rules;
   const int maxy = Y <= 32 ? 32 : Y <= 48 ? 48 : 64;
   const int rmax = n_rules <= 1 ? 1 : n_rules <= 4 ? 4 : 16;
@@ -358,6 +363,9 @@ static int jit_kernels(lt_ctx* c, const lt_index* f, int Y, const lt_params* prm
     sp.year_out = o->val_fit || o->fit_m || o->fit_b || o->right_m || o->right_b || o->spike ||
                   o->vertex;
     sp.params = *prm;
+    // the scene's tables too, unless LT_JIT_SCENE=0
+    static const bool scene_on = !(getenv("LT_JIT_SCENE") && getenv("LT_JIT_SCENE")[0] == '0');
+    if (scene_on) sp.scene = scene;
   }
   std::string err;
   const std::string src = lt_jit::source(f->prog, maxy, rmax, vt, sp, err);
@@ -405,7 +413,7 @@ static int launch_tile(lt_ctx* c, const lt_params* prm, const lt_tile_in* in,
   lt::TileLaunch l{c->d_scene, prm, in, out, c->d_xtab, dl, dn, yf, Y, c->device, stream};
   const lt_jit_kernels* jk = nullptr;
   if (in->obs_bands && in->index) {  // a program inlined into JIT kernels (lt_jit.h)
-    const int rc = jit_kernels(c, in->index, Y, prm, in, out, &jk);
+    const int rc = jit_kernels(c, in->index, Y, prm, in, out, c->h_scene, &jk);
     if (rc != LT_OK) return rc;
   }
   // the JIT kernels' one argument, as the product kernels get it (lt_kernels.h kernel_args)
@@ -539,8 +547,9 @@ int lt_analyze_tiles_after(lt_ctx* c, const lt_scene* sc, const lt_params* prm, 
     // an earlier call, possibly on another stream, may still be reading d_scene: its last tile's
     // resolve (side stream, in order, after every analyze it waited for) marks the end of all of
     // that work, so the copy waits for it
-    if (c->set_used[0] || c->set_used[1])
-      HIP_OR_FAIL(c, hipStreamWaitEvent(stream, c->ev_resolved[c->last_set], 0));
+    bool any = false;
+    for (int s = 0; s < lt_ctx::kSets; s++) any = any || c->set_used[s];
+    if (any) HIP_OR_FAIL(c, hipStreamWaitEvent(stream, c->ev_resolved[c->last_set], 0));
     HIP_OR_FAIL(c, hipEventSynchronize(c->scene_copied));  // staging buffer free again
     memcpy(c->h_scene, &tmp, sizeof tmp);
     HIP_OR_FAIL(c, hipMemcpyAsync(c->d_scene, c->h_scene, sizeof tmp, hipMemcpyHostToDevice,
@@ -549,7 +558,7 @@ int lt_analyze_tiles_after(lt_ctx* c, const lt_scene* sc, const lt_params* prm, 
     c->scene_valid = true;
   }
 
-  // deferred-pixel lists: two sets (tile t uses set t % 2), sized for the largest tile seen
+  // deferred-pixel lists: kSets sets (round robin over tiles), sized for the largest tile seen
   if (c->defer_cap < cap) {
     // a smaller list may still be read by an earlier call's resolve on the side stream
     if (c->side) HIP_OR_FAIL(c, hipStreamSynchronize(c->side));
@@ -557,10 +566,11 @@ int lt_analyze_tiles_after(lt_ctx* c, const lt_scene* sc, const lt_params* prm, 
     c->d_defer = nullptr;
     if (c->d_yflags) HIP_OR_FAIL(c, hipFree(c->d_yflags));
     c->d_yflags = nullptr;
-    HIP_OR_FAIL(c, hipMalloc((void**)&c->d_defer, 2 * 2 * sizeof(int64_t) * (size_t)cap));
-    HIP_OR_FAIL(c, hipMalloc((void**)&c->d_yflags, 2 * 2 * sizeof(uint64_t) * (size_t)cap));
+    const size_t ns = lt_ctx::kSets;
+    HIP_OR_FAIL(c, hipMalloc((void**)&c->d_defer, ns * 2 * sizeof(int64_t) * (size_t)cap));
+    HIP_OR_FAIL(c, hipMalloc((void**)&c->d_yflags, ns * 2 * sizeof(uint64_t) * (size_t)cap));
     if (!c->d_ndefer)
-      HIP_OR_FAIL(c, hipMalloc((void**)&c->d_ndefer, 2 * 4 * sizeof(unsigned long long)));
+      HIP_OR_FAIL(c, hipMalloc((void**)&c->d_ndefer, ns * 4 * sizeof(unsigned long long)));
     c->defer_cap = cap;
   }
   if (!c->side) {
@@ -574,18 +584,23 @@ int lt_analyze_tiles_after(lt_ctx* c, const lt_scene* sc, const lt_params* prm, 
     const char* pr = getenv("LT_RESOLVE_PRIORITY");
     const bool normal = pr && strcmp(pr, "normal") == 0;
     HIP_OR_FAIL(c, hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, normal ? 0 : least));
-    for (int s = 0; s < 2; s++) {
+    for (int s = 0; s < lt_ctx::kSets; s++) {
       HIP_OR_FAIL(c, hipEventCreateWithFlags(&c->ev_analyzed[s], hipEventDisableTiming));
       HIP_OR_FAIL(c, hipEventCreateWithFlags(&c->ev_resolved[s], hipEventDisableTiming));
     }
+    const char* ns = getenv("LT_DEFER_SETS");
+    if (ns && atoi(ns) >= 2 && atoi(ns) <= lt_ctx::kSets) c->n_sets = atoi(ns);
   }
   // Tile t: analyze on `stream`, resolve on the context's side stream, so tile t's resolve runs
-  // beside tile t+1's analyze (the resolve is a few long waves: latency, not throughput). Set
-  // t % 2 is reused by tile t+2 only after tile t's resolve; at the end `stream` waits for the
-  // last resolve, so every output is complete in `stream` order when the call's work is done.
+  // beside tile t+1's analyze (the resolve is a few long waves: latency, not throughput). A set
+  // is reused n_sets tiles later, after its tile's resolve: with two sets tile t+2's analyze
+  // waited for tile t's resolve, whose waves get CU slots only in tile t+1's drain (kernel trace
+  // r04_run1: 0.37 ms of a 22 ms step with the GPU nearly idle). At the end `stream` waits for
+  // the last resolve, so every output is complete in `stream` order when the call's work is done.
   for (int t = 0; t < n_tiles; t++) {
     if (ins[t].n_pix == 0) continue;
-    const int set = t & 1;
+    const int set = c->next_set;
+    c->next_set = (set + 1) % c->n_sets;
     if (c->set_used[set]) HIP_OR_FAIL(c, hipStreamWaitEvent(stream, c->ev_resolved[set], 0));
     if (ready && ready[t]) HIP_OR_FAIL(c, hipStreamWaitEvent(stream, (hipEvent_t)ready[t], 0));
     const int rc = launch_tile(c, prm, &ins[t], &outs[t], Y, stream, c->side, set);

@@ -27,6 +27,12 @@
 #ifndef LT_RESOLVE_PRIV_MAXY
 #define LT_RESOLVE_PRIV_MAXY 48
 #endif
+// the resolve stage's DP: 1 = the exact-OPT DP over every column (the default), 0 = the lazy DP
+// with every ambiguous column decided exactly where it arises (c2 resolve 0.63 vs 0.44 ms per
+// launch, 2528 vs 2584 Mpx/s, profiles/r04_run13: the stage is latency-bound, not LAPACK-bound)
+#ifndef LT_RESOLVE_FULL
+#define LT_RESOLVE_FULL 1
+#endif
 // labels-only launches of up to this many rules take the certified path (closed-form fits, the
 // emulated ones only around the rules' candidates); more rules keep one emulated fit per vertex
 #ifndef LT_CERT_RULES
@@ -132,8 +138,10 @@ struct WaveLds {
 // EXACT = false (analyze stage): the lazy DP; returns kDeferExact when the pixel's optimal path
 // crosses an ambiguous DP column, kDeferWide when its values are not exact in binary32 (the
 // resolve stage redoes them with binary32 / binary64 LDS series), else kDone.
-// EXACT = true (resolve stage): the exact-OPT DP, every column decided with the emulated LAPACK
-// residual of each start inside the error window; always kDone.
+// EXACT = true (resolve stage): the same lazy DP, but a column its intervals cannot decide is
+// decided on the spot with the emulated LAPACK residuals of the candidates (and of the links of
+// their optimal prefixes whose values are not yet exact); always kDone. (LT_RESOLVE_FULL: the
+// exact-OPT DP over every column instead.)
 enum { kDone = 0, kDeferExact = 1, kDeferWide = 2 };
 
 // Phase probe of analyze_fast: probe.mark(k) is called by every lane at the end of phase k
@@ -148,11 +156,18 @@ struct NoProbe {
 };
 
 template <int MAXY, int RMAX, bool EXACT, class VT, class Probe = NoProbe>
-__device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const lt_tile_in& in,
+__device__ inline int analyze_fast(const DevScene& S_launch, const lt_params& P, const lt_tile_in& in,
                                    const lt_tile_out& out, const lsq_xf* __restrict__ xtab,
                                    uint64_t* __restrict__ yflags, int64_t p, bool live, int lane,
                                    WaveLds<MAXY, VT, EXACT>& L,
                                    const Probe& probe = Probe()) {
+  // the scene: constants of a JIT kernel specialised for it (lt_jit.h), else the launch's
+#ifdef LT_SPEC_SCENE
+  const DevScene& S = lt_spec_scene;
+  (void)S_launch;
+#else
+  const DevScene& S = S_launch;
+#endif
 #ifdef LT_SPEC_Y
   constexpr int Y = LT_SPEC_Y;
 #else
@@ -616,7 +631,7 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
     if constexpr (EXACT) return L.ag[j][lane];
     else return AG[j];
   };
-  if constexpr (EXACT) {
+  if constexpr (EXACT && LT_RESOLVE_FULL != 0) {
     if constexpr (MAXY <= LT_RESOLVE_PRIV_MAXY) {
       // ---- exact-OPT DP: closed-form intervals, then the emulated LAPACK residual for every
       // start whose interval reaches the column's smallest upper bound; first exact minimum ----
@@ -837,6 +852,83 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
     const bool zok = c > 0.0;
     const bool zlane = zok && intdata;
     uint64_t amb = 0;
+    // resolve stage: the exact decision of column j for the lanes xr (see column below). One
+    // lockstep loop of emulated residuals: per lane first the links k (OPTa[k] = fl(fl(e(a, k-1) +
+    // c) + OPTa[a]), a = argmin of column k-1) that the candidates' OPT values need, in increasing
+    // k, then the candidates in increasing start order (strict "<": the first minimum)
+    auto resolve_column = [&](const int j, const bool xr, const double H, uint64_t cs,
+                              const double opt_j, const int tg_j, const double opt_jm1,
+                              const int tg_jm1, int& a, double& vnew) {
+      // the 1- and 2-point starts j, j-1 (residual 0), when their interval reaches H
+      {
+        const double v0 = c + opt_j;
+        const double w0 = tg_j < 256 ? 0.0 : __builtin_fma(0x1p-50, __builtin_fabs(v0), Emax);
+        if (!(v0 - w0 > H)) cs |= 1ull << j;
+        if (j >= 1) {
+          const double v1s = c + opt_jm1;
+          const double w1 =
+              tg_jm1 < 256 ? 0.0 : __builtin_fma(0x1p-50, __builtin_fabs(v1s), Emax);
+          if (!(v1s - w1 > H)) cs |= 1ull << (j - 1);
+        }
+      }
+      if (!xr) cs = 0;
+      uint64_t need = cs & ~exact;  // OPTa entries to make exact, with their prefixes' links
+      {
+        const int top = wave_max(need ? 63 - __builtin_clzll(need) : 0);
+        for (int kk = top; kk >= 1; kk--) {
+          const int k = __builtin_amdgcn_readfirstlane(kk);
+          if ((need >> k) & 1) {
+            const int b = L.ag[k - 1][lane];
+            if (!((exact >> b) & 1)) need |= 1ull << b;
+          }
+        }
+      }
+      const int steps = wave_max(__builtin_popcountll(need) + __builtin_popcountll(cs));
+      double best = inf;
+      int bi = 0;
+      for (int r = 0; r < steps; r++) {
+        const bool link = need != 0;
+        const bool act = link || cs != 0;
+        int i = 0, m = 0;  // the segment: points i .. i+m-1
+        int k = 0;
+        if (link) {
+          k = __builtin_ctzll(need);
+          need &= need - 1;
+          i = L.ag[k - 1][lane];
+          m = k - i;
+        } else if (act) {
+          i = __builtin_ctzll(cs);
+          cs &= cs - 1;
+          m = j - i + 1;
+        }
+        const bool ls = act && m >= 3;
+        double e = 0.0;
+        if (__ballot(ls)) {
+          double sm, sb, ssr;
+          const int rc = lsq_lockstep(
+              ls, m, [&](int q) { return (int)L.xn[i + q][lane]; },
+              [&](int q) { return (double)L.ys[i + q][lane]; }, xtab, false, true, sm, sb, ssr);
+          if (ls) {
+            if (rc < 0) status |= LT_ST_NUMERIC;
+            e = ssr;
+          }
+        }
+        if (act) {
+          const double v = (e + c) + OPTa[i];  // per-lane index: exact by now
+          if (link) {
+            OPTa[k] = v;
+            exact |= 1ull << k;
+          } else if (v < best) {
+            best = v;
+            bi = i;
+          }
+        }
+      }
+      if (xr) {
+        a = bi;
+        vnew = best;
+      }
+    };
     // column j: wx0 receives point j (its slot held point j-4); wx1..wx3 hold points j-1..j-3;
     // opt_j..opt_jm3 hold OPTa[j..j-3] (tags tg_*), and OPTa[j+1] is written over opt_jm3
     auto column = [&](const int j, int& wx0, int& wx1, int& wx2, int& wx3, double& wy0,
@@ -852,6 +944,7 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
       // interval enters the trackers at the end of the column)
       double Ve = inf, Hi = inf, L1 = inf, L2 = inf, v1 = inf, gv = inf;
       int ie = 0, i1 = 0, iL = -1, n1 = -1, gi = -1, gt = 0;
+      uint64_t cand = 0;  // resolve stage: the >= 3-point starts an exact decision prices
       // (the bounds Hi, L1, L2 are only compared: v_min_f64 instead of a select pair; the values
       // that become OPTa, v1 and Ve, are selected)
       auto track = [&](int i, double v, double hi, double lo, int nt) __attribute__((always_inline)) {
@@ -995,6 +1088,11 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
       auto one_start = [&](int i, double o, int tg) __attribute__((always_inline)) {
         double v, hi, lo, bnd;
         const bool nz = price(i, o, tg, v, hi, lo, bnd);
+        // resolve stage: every start whose interval reaches the column's current upper bound (a
+        // NaN bound included) is a candidate of an exact decision
+        if constexpr (EXACT) {
+          if (!(lo > upper())) cand |= 1ull << i;
+        }
         if (__ballot(lo <= upper())) {
           bool zr = false;
           if (__ballot(nz)) zr = nz && zero_test(j - i + 1, Sx, Sxx, Sy, Sxy, Syy);
@@ -1033,6 +1131,7 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
       const double H = __builtin_fmin(Hi, Ve);  // the exact minimum lies in [min(L1, Ve), H]
       int a, tnew;
       double vnew, enew = 0.0;
+      bool xres = false;  // resolve stage: this lane decides the column exactly
       if (L1 > H) {  // no inexact interval reaches H: the exact candidates decide
         a = ie;
         vnew = Ve;
@@ -1045,12 +1144,26 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
         // its half-width, rounded up: Hi = fl(v1 + w1) >= v1 + w1 - ulp(Hi) / 2
         enew = __builtin_fma(Hi - v1, 1.0 + 0x1p-50, 0x1p-50 * __builtin_fabs(Hi));
       } else {
-        if (col) amb |= 1ull << j;
+        if constexpr (EXACT) xres = col;
+        else if (col) amb |= 1ull << j;
         a = v1 <= Ve ? i1 : ie;
         vnew = v1 <= Ve ? v1 : Ve;
         tnew = (j + 1) << 8;
         const double Lo = __builtin_fmin(L1, Ve);
         enew = (H - Lo) * (1.0 + 0x1p-40) + 0x1p-50 * __builtin_fabs(vnew);
+      }
+      if constexpr (EXACT) {
+        // resolve stage: an ambiguous column is decided exactly here, so no interval widens
+        // Emax and the next columns keep their certified decisions. The candidates are the
+        // starts whose interval reaches H; each is worth fl(fl(e + c) + OPT[i]) with e the
+        // emulated LAPACK residual (0 for 1-2 points) and OPT[i] the reference value: where OPTa[i]
+        // is not exact yet, the links of its optimal prefix (argmins of decided columns, each
+        // the reference's) are priced first, in increasing order, each made exact once.
+        if (__ballot(xres)) resolve_column(j, xres, H, cand, opt_j, tg_j, opt_jm1, tg_jm1, a, vnew);
+        if (xres) {
+          tnew = 0;
+          enew = 0.0;
+        }
       }
       if (col) {
         ag_set(j, a);
@@ -1061,6 +1174,34 @@ __device__ inline int analyze_fast(const DevScene& S, const lt_params& P, const 
         tg_jm3 = tnew;
       }
     };
+    if constexpr (EXACT) {
+      // resolve stage: one column per iteration (its exact decisions are code the unrolled loop
+      // below would hold four times), the window rotated by register moves
+      for (int jj = 0; jj < nmax; jj++) {
+        const int j = __builtin_amdgcn_readfirstlane(jj);
+        column(j, xA, xB, xC, xD, yA, yB, yC, yD, oA, oB, oC, oD, gA, gB, gC, gD);
+        const int xt = xD;
+        xD = xC;
+        xC = xB;
+        xB = xA;
+        xA = xt;
+        const double yt = yD;
+        yD = yC;
+        yC = yB;
+        yB = yA;
+        yA = yt;
+        const double ot = oD;
+        oD = oC;
+        oC = oB;
+        oB = oA;
+        oA = ot;
+        const int gt = gD;
+        gD = gC;
+        gC = gB;
+        gB = gA;
+        gA = gt;
+      }
+    } else
     for (int jj = 0; jj < nmax; jj += 4) {
       const int j = __builtin_amdgcn_readfirstlane(jj);  // column index in an SGPR
       column(j, xA, xB, xC, xD, yA, yB, yC, yD, oA, oB, oC, oD, gA, gB, gC, gD);

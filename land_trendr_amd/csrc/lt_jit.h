@@ -29,6 +29,7 @@
 #include <vector>
 
 #include "lt_index.h"
+#include "lt_pixel.h"
 
 struct lt_jit_kernels {
   hipModule_t mod = nullptr;
@@ -113,7 +114,25 @@ struct Spec {
   int n_years = 0;
   bool masked = false, year_out = false;
   lt_params params{};
+  const lt::DevScene* scene = nullptr;  // the scene's tables as constants (LT_SPEC_SCENE)
 };
+
+// a DevScene as a C++ initializer (the arrays up to their used length; the rest zero-fills)
+inline std::string fmt_scene(const lt::DevScene& S) {
+  std::string r = "{" + std::to_string(S.n_obs) + ", " + std::to_string(S.n_years) + ", " +
+                  std::to_string((unsigned long long)S.feb29_mask) + "ull";
+  auto arr = [&](const int32_t* a, int n) {
+    r += ", {";
+    for (int i = 0; i < n; i++) r += (i ? "," : "") + std::to_string(a[i]);
+    r += "}";
+  };
+  arr(S.year, S.n_years);
+  arr(S.slot_begin, S.n_years + 1);
+  arr(S.order, S.n_obs);
+  arr(S.dist, S.n_obs);
+  arr(S.winner_all, S.n_years);
+  return r + "}";
+}
 
 inline std::string fmt_rule(const lt_rule& r) {
   char b[256];
@@ -135,6 +154,20 @@ inline std::string source(const lt_index_prog& P, int maxy, int rmax, const char
   src += lt_idx::kPrelude;
   snprintf(head, sizeof head, "#define LT_JIT_INDEX 1\n#define LT_JIT_BAND_T %s\n", BT);
   src += head;
+  // A/B runs: LT_JIT_DEFINES="NAME=VALUE,NAME2=VALUE2" adds compile-time switches of the kernel
+  // headers (LT_RESOLVE_FULL, LT_WB, ...) to the generated source (and so to its cache key)
+  if (const char* e = getenv("LT_JIT_DEFINES")) {
+    std::string s(e);
+    size_t at = 0;
+    while (at < s.size()) {
+      size_t end = s.find(',', at);
+      if (end == std::string::npos) end = s.size();
+      std::string d = s.substr(at, end - at);
+      const size_t eq = d.find('=');
+      if (!d.empty()) src += "#define " + (eq == std::string::npos ? d : d.substr(0, eq) + " " + d.substr(eq + 1)) + "\n";
+      at = end + 1;
+    }
+  }
   if (sp.on) {
     const lt_params& Q = sp.params;
     char d[512];
@@ -150,6 +183,10 @@ inline std::string source(const lt_index_prog& P, int maxy, int rmax, const char
     for (int r = 0; r < (Q.n_rules > 0 ? Q.n_rules : 1); r++)
       src += (r ? ", " : "") + fmt_rule(Q.rules[r]);
     src += "};\n";
+  }
+  if (sp.on && sp.scene) {
+    src += "#include \"lt_pixel.h\"\n#define LT_SPEC_SCENE 1\n";
+    src += "__device__ constexpr lt::DevScene lt_spec_scene = " + fmt_scene(*sp.scene) + ";\n";
   }
   src += "__device__ inline double lt_jit_index(const LT_JIT_BAND_T* b, long long band_stride) {\n";
   src += body;

@@ -67,12 +67,19 @@ __device__ inline void analyze_body() {
 }
 
 // Stage 2 (wave-lockstep, lt_fast.h with EXACT): the deferred pixels (list n_defer[0] of
-// `defer`), exact-OPT DP. A grid of exactly the resident waves takes 64-pixel groups of the list from a
-// counter (group cost varies a lot); every wave leaves once the counter has passed the list.
+// `defer`). A grid of exactly the resident waves takes groups of LT_RESOLVE_GROUP pixels of the
+// list from a counter (group cost varies a lot); every wave leaves once the counter has passed the
+// list. A group smaller than the wave leaves lanes idle but splits the list finer: the stage is a
+// few thousand latency-bound waves, so its time is that of its slowest wave.
 // For an int16 series the list of values binary32 cannot hold ([n_pix, 2 n_pix)) is empty.
+#ifndef LT_RESOLVE_GROUP
+#define LT_RESOLVE_GROUP 64
+#endif
 template <int MAXY, int RMAX, class VT>
 __device__ inline void resolve_body() {
   __shared__ WaveLds<MAXY, VT, true> L;
+  constexpr int G = LT_RESOLVE_GROUP;
+  static_assert(G >= 1 && G <= 64, "a group is at most one wave");
   const int lane = threadIdx.x;
   const KernelArgs& K = args();
   unsigned long long* counters = K.n_defer;
@@ -81,10 +88,10 @@ __device__ inline void resolve_body() {
     unsigned g = 0;
     if (lane == 0) g = atomicAdd((unsigned*)&counters[1], 1u);
     g = __builtin_amdgcn_readfirstlane(__shfl(g, 0));
-    const int64_t base = (int64_t)g * 64;
+    const int64_t base = (int64_t)g * G;
     if (base >= n) break;
     const int64_t k = base + lane;
-    const bool live = k < n;
+    const bool live = lane < G && k < n;
     const KernelArgs& Kk = args();
     analyze_fast<MAXY, RMAX, true, VT>(*Kk.S, Kk.P, Kk.in, Kk.out, Kk.xtab, Kk.yflags,
                                        live ? Kk.defer[k] : 0, live, lane, L);
