@@ -33,6 +33,15 @@
 #ifndef LT_RESOLVE_FULL
 #define LT_RESOLVE_FULL 1
 #endif
+// timing-only attribution builds (wrong outputs; A/B runs through LT_JIT_DEFINES):
+// LT_AB_NO_YEAR_STORES = 1 drops the year-major loop's per-year plane stores, 2 also the winner
+// pick's val_raw / winner rows; LT_AB_NO_FITS = 1 drops the year-major loop's emulated fits
+#ifndef LT_AB_NO_YEAR_STORES
+#define LT_AB_NO_YEAR_STORES 0
+#endif
+#ifndef LT_AB_NO_FITS
+#define LT_AB_NO_FITS 0
+#endif
 // labels-only launches of up to this many rules take the certified path (closed-form fits, the
 // emulated ones only around the rules' candidates); more rules keep one emulated fit per vertex
 #ifndef LT_CERT_RULES
@@ -399,7 +408,8 @@ __device__ inline int analyze_fast(const DevScene& S_launch, const lt_params& P,
       const int y = yb + u;
       if (y >= Y || !live) continue;
       const int64_t q = (int64_t)y * os + p;
-      if (out.winner) __builtin_nontemporal_store((int16_t)best[u], out.winner + q);
+      if (out.winner && LT_AB_NO_YEAR_STORES < 2)
+        __builtin_nontemporal_store((int16_t)best[u], out.winner + q);
       if (best[u] >= 0) {
         if ((S.feb29_mask >> y) & 1) status |= LT_ST_FEB29;
         const double v = val[u];
@@ -423,8 +433,8 @@ __device__ inline int analyze_fast(const DevScene& S_launch, const lt_params& P,
         }
         pres |= 1ull << y;
         T++;
-        if (out.val_raw) __builtin_nontemporal_store(v, out.val_raw + q);
-      } else if (out.val_raw) {  // the other per-year planes: the year-major output loop
+        if (out.val_raw && LT_AB_NO_YEAR_STORES < 2) __builtin_nontemporal_store(v, out.val_raw + q);
+      } else if (out.val_raw && LT_AB_NO_YEAR_STORES < 2) {  // the other per-year planes: the year-major output loop
         __builtin_nontemporal_store(nan, out.val_raw + q);
       }
     }
@@ -1273,6 +1283,37 @@ __device__ inline int analyze_fast(const DevScene& S_launch, const lt_params& P,
     // year_flags_kernel (lt_abi.hip) in 256-byte rows instead of 64-byte pieces here
     uint64_t spk = 0, vtx = 0;
     int t = 0, k = 0, q = 0;         // present index, non-spike index, vertex number
+    // One year's row of the five binary64 planes. (A fit step's x-set table loads share the
+    // in-order vector-memory counter with the stores, so a load issued after a year's stores waits
+    // for all of them (s_waitcnt vmcnt(0)); holding each row a year or two and storing it after
+    // the next fit step spilled the held rows: c5 1060 / 928 vs 1260 Mpx/s, profiles/r04_run16.)
+    struct Row {
+      double fv, fm, fb, rm, rb;
+      bool pr;  // the year is present in this lane
+      bool uni;  // ... in every emitting lane (no NaN selects)
+    };
+    auto store_row = [&](int yy, const Row& r) __attribute__((always_inline)) {
+      const int64_t o = (int64_t)yy * os + p;
+      // write-once planes: nontemporal stores (same-box c5 A/B: 1012 vs 896-925 Mpx/s). When
+      // the year is present in every emitting lane (always, without a cloud mask) the values
+      // are stored as they are: no NaN select pair per plane
+      auto put = [&](double* plane, double v) __attribute__((always_inline)) {
+        if (plane && !LT_AB_NO_YEAR_STORES) __builtin_nontemporal_store(v, plane + o);
+      };
+      if (r.uni) {
+        put(out.val_fit, r.fv);
+        put(out.fit_m, r.fm);
+        put(out.fit_b, r.fb);
+        put(out.right_m, r.rm);
+        put(out.right_b, r.rb);
+      } else {
+        put(out.val_fit, r.pr ? r.fv : nan);
+        put(out.fit_m, r.pr ? r.fm : nan);
+        put(out.fit_b, r.pr ? r.fb : nan);
+        put(out.right_m, r.pr ? r.rm : nan);
+        put(out.right_b, r.pr ? r.rb : nan);
+      }
+    };
     for (int y = 0; y < Y; y++) {    // wave-uniform
       const bool pr = good && ((pres >> y) & 1);
       const bool sp = pr && ((spike >> t) & 1);
@@ -1281,7 +1322,7 @@ __device__ inline int analyze_fast(const DevScene& S_launch, const lt_params& P,
       const bool nextfit = isv && after != 0;
       double sm = 0.0, sbv = 0.0;
       bool fitnow = false;
-      if (__ballot(nextfit && !have_n)) {
+      if (__ballot(nextfit && !have_n) && !LT_AB_NO_FITS) {
         const uint64_t fnext = frem & (frem - 1);
         fitnow = fnext != 0 && (!have_n || nextfit);
         const int kbase = fitnow ? __builtin_ctzll(frem) : 0;
@@ -1307,6 +1348,7 @@ __device__ inline int analyze_fast(const DevScene& S_launch, const lt_params& P,
         nm = sm;
         nb = sbv;
       }
+
       if (isv && !nextfit) {  // the last vertex: left eqn = right eqn = the previous one
         pm = cm;
         pb = cb;
@@ -1327,27 +1369,12 @@ __device__ inline int analyze_fast(const DevScene& S_launch, const lt_params& P,
         vrem = after;
         q++;
       }
-      if (emit) {  // absent years and pixels the reference raises for: NaN / 0
+      {  // absent years and pixels the reference raises for: NaN / 0
+        const Row row{fv, fmv, fbv, cm, cb, pr, __ballot(emit && !pr) == 0};
+        if (emit) store_row(y, row);
+      }
+      if (emit) {
         const int64_t o = (int64_t)y * os + p;
-        // write-once planes: nontemporal stores (same-box c5 A/B: 1012 vs 896-925 Mpx/s). When
-        // the year is present in every emitting lane (always, without a cloud mask) the values
-        // are stored as they are: no NaN select pair per plane
-        auto put = [&](double* plane, double v) __attribute__((always_inline)) {
-          if (plane) __builtin_nontemporal_store(v, plane + o);
-        };
-        if (__ballot(!pr) == 0) {
-          put(out.val_fit, fv);
-          put(out.fit_m, fmv);
-          put(out.fit_b, fbv);
-          put(out.right_m, cm);
-          put(out.right_b, cb);
-        } else {
-          put(out.val_fit, pr ? fv : nan);
-          put(out.fit_m, pr ? fmv : nan);
-          put(out.fit_b, pr ? fbv : nan);
-          put(out.right_m, pr ? cm : nan);
-          put(out.right_b, pr ? cb : nan);
-        }
         if (yflags) {
           spk |= (uint64_t)sp << y;
           vtx |= (uint64_t)isv << y;

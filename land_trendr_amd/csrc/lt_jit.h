@@ -196,9 +196,14 @@ inline std::string source(const lt_index_prog& P, int maxy, int rmax, const char
   const char* we = getenv("LT_JIT_WAVES");
   const int waves = we && atoi(we) >= 1 && atoi(we) <= 8 ? atoi(we) : 4;
   char k[1024];
+  // phase cuts (timing-only A/B runs, wrong outputs): LT_JIT_DEFINES=LT_JIT_STOP_AFTER=k ends
+  // every pixel after phase k of lt_fast.h (0 winner pick, 1 despike, 2 DP, 3 fits + output)
+  src += "#ifdef LT_JIT_STOP_AFTER\nstruct lt_jit_probe { static constexpr int kStopAfter = "
+         "LT_JIT_STOP_AFTER; __device__ void mark(int) const {} };\n#else\n"
+         "using lt_jit_probe = lt::NoProbe;\n#endif\n";
   snprintf(k, sizeof k,
            "extern \"C\" __global__ __launch_bounds__(64, %d) void lt_jit_analyze(const "
-           "lt::KernelArgs A) {\n  (void)A;\n  lt::analyze_body<%d, %d, %s, lt::NoProbe>();\n}\n"
+           "lt::KernelArgs A) {\n  (void)A;\n  lt::analyze_body<%d, %d, %s, lt_jit_probe>();\n}\n"
            "extern \"C\" __global__ __launch_bounds__(64, 4) void lt_jit_resolve(const "
            "lt::KernelArgs A) {\n  (void)A;\n  lt::resolve_body<%d, %d, %s>();\n}\n",
            waves, maxy, rmax, vt, maxy, rmax, vt);
