@@ -1292,6 +1292,8 @@ __device__ inline int analyze_fast(const DevScene& S_launch, const lt_params& P,
       bool pr;  // the year is present in this lane
       bool uni;  // ... in every emitting lane (no NaN selects)
     };
+    // (16-byte stores of pixel pairs from the even lanes, the odd lane's value moved over by DPP:
+    // c5 1083-1092 vs 1260 Mpx/s, profiles/r04_run19)
     auto store_row = [&](int yy, const Row& r) __attribute__((always_inline)) {
       const int64_t o = (int64_t)yy * os + p;
       // write-once planes: nontemporal stores (same-box c5 A/B: 1012 vs 896-925 Mpx/s). When
