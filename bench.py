@@ -316,7 +316,8 @@ def main():
     ap.add_argument('--config', default='c2', choices=sorted(CONFIGS))
     ap.add_argument('--pixels', type=int, default=0, help='pixels per scene (default: config)')
     ap.add_argument('--tile', type=int, default=0,
-                    help='pixels per tile (0: 1<<24, or scene/8 for the c4 mosaic)')
+                    help='pixels per tile (0: the whole scene for a labels-only config on one '
+                         'GPU, else 1<<24; scene/8 for the c4 mosaic)')
     ap.add_argument('--no-gather', action='store_true',
                     help='N>1: skip the exchange of label rasters to rank 0')
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
@@ -365,7 +366,12 @@ def main():
         tile = args.tile or ((P + 7) // 8 + 63) // 64 * 64
         mosaic = Mosaic([P] * cfg['scenes'], tile, world, rank, 'round_robin')
     else:  # one scene per rank (weak scaling)
-        tile = args.tile or (1 << 24)
+        # one launch per scene on one GPU for the labels-only configs (fewer launch drains and
+        # resolve launches: c2 2619-2630 vs 2577-2592, c3 1995 vs 1971 Mpx/s with 16.8 Mpx tiles,
+        # profiles/r04_run23); 16.8 Mpx tiles when the writer's label exchange can overlap the
+        # next tile (N > 1) or the config writes the per-year planes
+        whole = world == 1 and not cfg['trendline'] and P <= (1 << 26)
+        tile = args.tile or (P if whole else (1 << 24))
         mosaic = Mosaic([P] * world, tile, world, rank, 'by_scene')
     fused = os.environ.get('LT_FUSED_INDEX', '1') != '0'
     items = mosaic_inputs(mosaic, cfg['years'], cfg['k'][0], cfg['k'][1], cfg['mask'],
@@ -460,12 +466,30 @@ def main():
     if args.e2e_steps > 0:
         if dist is not None:
             dist.barrier()
-        dt, bh, bd = end_to_end(runner, cfg, args.e2e_steps)
+        e2e_runner, e2e_tile = runner, mosaic.tile
+        if not mosaic_cfg and mosaic.tile > (1 << 24):
+            # the bands cross PCIe per tile, overlapped with the previous tile's kernels: a
+            # whole-scene tile would leave the copy unhidden, so these steps use 16.8 Mpx tiles
+            m2 = Mosaic([P] * world, 1 << 24, world, rank, 'by_scene')
+            items2 = mosaic_inputs(m2, cfg['years'], cfg['k'][0], cfg['k'][1], cfg['mask'],
+                                   cfg['seed'], dev, TARGET,
+                                   band_layout=os.environ.get('LT_BAND_LAYOUT',
+                                                              'pixel' if fused else 'planar'),
+                                   mask_format=os.environ.get('LT_MASK_FORMAT', 'bits'))
+            e2e_runner = MosaicRunner(eng, m2, params, items2, fields, index_fn, dist,
+                                      exchange_fields=() if args.no_gather else
+                                      ('class_val', 'onset_year', 'duration', 'magnitude'),
+                                      load_stream=not args.serial_load, group=args.group)
+            e2e_runner.step()  # warm
+            torch.cuda.synchronize()
+            e2e_tile = m2.tile
+        dt, bh, bd = end_to_end(e2e_runner, cfg, args.e2e_steps)
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         if dist is not None:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
         e2e = {'value': round(mosaic.n_pix * args.e2e_steps / dt / 1e6, 3), 'unit': 'Mpixels/s',
+               'tile_pixels': e2e_tile,
                'ms_per_step': round(dt / args.e2e_steps * 1e3, 3), 'steps': args.e2e_steps,
                'h2d_bytes_per_step_rank0': bh // args.e2e_steps,
                'd2h_bytes_per_step_rank0': bd // args.e2e_steps,
