@@ -497,12 +497,18 @@ __device__ inline int analyze_fast(const DevScene& S_launch, const lt_params& P,
     int last_good = ok ? (int)L.ys[0][lane] : 0;
     int xv = last_good, yv = ok ? (int)L.ys[1][lane] : 0;
     if (ok) n = 1;  // point 0 is never a spike (its offset, 0, is in place)
+    const int nK = -K;
     for (int t0 = 1; t0 < Tmax; t0 += 8) {
       int z[8], xo[8];
+      // unconditional LDS reads (the slot index clamped into the arrays; a value past the
+      // lane's T is never used): a guarded read per slot cost a scalar branch and a
+      // condition moved through a VGPR each
 #pragma unroll
       for (int u = 0; u < 8; u++) {
-        z[u] = t0 + u + 1 < Tmax ? (int)L.ys[t0 + u + 1][lane] : 0;
-        xo[u] = t0 + u < Tmax ? (int)L.xn[t0 + u][lane] : 0;
+        const int tz = t0 + u + 1 < MAXY ? t0 + u + 1 : MAXY - 1;
+        const int tx = t0 + u < MAXY ? t0 + u : MAXY - 1;
+        z[u] = (int)L.ys[tz][lane];
+        xo[u] = (int)L.xn[tx][lane];
       }
 #pragma unroll
       for (int u = 0; u < 8; u++) {
@@ -514,12 +520,10 @@ __device__ inline int analyze_fast(const DevScene& S_launch, const lt_params& P,
         if (t + 1 < T) {  // the last point is never a spike
           const int zv = z[u];
           const int d1 = yv - xv, d2 = zv - yv;
-          // monotone <=> sign(d1) * sign(d2) >= 0
-          const int s1 = d1 < -1 ? -1 : (d1 > 1 ? 1 : d1), s2 = d2 < -1 ? -1 : (d2 > 1 ? 1 : d2);
-          const bool mono = __mul24(s1, s2) >= 0;
-          const int ad = __builtin_abs(d1) < __builtin_abs(d2) ? __builtin_abs(d1)
-                                                                : __builtin_abs(d2);
-          is_spike = !mono && ad >= K && yv != last_good;
+          // not monotone (x <= y <= z or x >= y >= z fails: the steps have strictly opposite
+          // signs) with both |steps| >= K: as K >= 1, one step >= K and the other <= -K
+          const bool big = (d1 >= K && d2 <= nK) || (d1 <= nK && d2 >= K);
+          is_spike = big && yv != last_good;
           if (!is_spike) last_good = yv;
           xv = yv;
           yv = zv;
@@ -528,10 +532,9 @@ __device__ inline int analyze_fast(const DevScene& S_launch, const lt_params& P,
           spike |= 1ull << t;
           continue;
         }
-        if (n != t) {
-          L.ys[n][lane] = (VT)cur;
-          L.xn[n][lane] = (uint8_t)xo[u];
-        }
+        // (slot n = t before the first spike: the same values rewritten, no branch)
+        L.ys[n][lane] = (VT)cur;
+        L.xn[n][lane] = (uint8_t)xo[u];
         n++;
       }
     }
