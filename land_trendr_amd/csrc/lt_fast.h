@@ -69,6 +69,14 @@
 
 namespace lt {
 
+// m * Sxx - Sx^2 of a segment's x sums (m <= 64 points, x <= 255: both products below 2^32, the
+// factors below 2^24) with two full-rate 24-bit multiplies instead of two v_mul_lo_u32 (the
+// analyze stage's lazy DP; in the resolve stage's exact DP as well it slowed c5's resolve,
+// profiles/r04_run27)
+__device__ inline int dmul24(int m, int sxx, int sx) {
+  return (int)(__umul24((unsigned)m, (unsigned)sxx) - __umul24((unsigned)sx, (unsigned)sx));
+}
+
 // max over the 64 lanes of a wave (every lane must call it). readfirstlane makes the result an
 // SGPR value, so loops bounded by it are wave-uniform to the compiler: scalar branches instead
 // of exec-mask juggling for every test on the loop counter.
@@ -1046,7 +1054,7 @@ __device__ inline int analyze_fast(const DevScene& S_launch, const lt_params& P,
         // closed-form SSE: (m*Syy - Sy^2 - N1^2/D) / m, one reciprocal
         const int m = j - i + 1;  // wave-uniform, >= 3
         const double md = (double)m;
-        const double D = (double)(m * Sxx - Sx * Sx);
+        const double D = (double)dmul24(m, Sxx, Sx);
         const double t1 = __builtin_fma(md, Syy, -(Sy * Sy));
         const double N1 = __builtin_fma(md, Sxy, -((double)Sx * Sy));
         const double den = md * D;
@@ -1069,7 +1077,7 @@ __device__ inline int analyze_fast(const DevScene& S_launch, const lt_params& P,
       auto zero_test = [&](int m, int sx, int sxx, double sy, double sxy, double syy)
                            __attribute__((always_inline)) {
         const double md = (double)m;
-        const double D = (double)(m * sxx - sx * sx);
+        const double D = (double)dmul24(m, sxx, sx);
         const double t1 = __builtin_fma(md, syy, -(sy * sy));
         const double N1 = __builtin_fma(md, sxy, -((double)sx * sy));
         return kZero * syy < 0x1p-54 * c && sse_exact_zero(t1, D, N1);
