@@ -12,7 +12,8 @@ Prints one progress line per chunk and writes a JSON summary.
 Usage (GPU box): python tests/full_scene_check.py --config c2 --out gpurun_out/full_c2.json
 (--first/--last: re-analyse one pixel range of the scene, to split a long check over calls;
 --labels-only: only the label rasters, as bench.py requests them for c2/c3, so the analyze kernel
-takes its certified labels-only path)
+takes its certified labels-only path; --whole --bench-fields: bench.py's exact timed launch on
+one GPU, the whole scene as one tile with bench's fields)
 """
 import argparse
 import json
@@ -49,18 +50,24 @@ def main():
     ap.add_argument('--labels-only', action='store_true',
                     help="the bench's own fields (label rasters only, the analyze kernel's "
                          "certified labels path) instead of adding val_fit / vertex")
+    ap.add_argument('--whole', action='store_true',
+                    help="bench.py's exact launch on one GPU for a labels-only config: the whole "
+                         "scene as one tile (one analyze launch, one resolve launch)")
+    ap.add_argument('--bench-fields', action='store_true',
+                    help="exactly bench.py's output fields (with --labels-only: without "
+                         "initial_val), so the kernel instance is the one bench.py times")
     ap.add_argument('--out', default='')
     args = ap.parse_args()
     c = bench.CONFIGS[args.config]
     P = args.pixels or c['pixels']
     if args.labels_only:
-        fields = LABELS + ('initial_val',)
+        fields = LABELS if args.bench_fields else LABELS + ('initial_val',)
     else:
         fields = LABELS + (tuple(bench.TRENDLINE_FIELDS) if c['trendline'] else
                            ('val_fit', 'vertex'))
     t0 = time.time()
     eng = get_engine(0)
-    m = Mosaic([P], 1 << 24, 1, 0, 'by_scene')
+    m = Mosaic([P], P if args.whole else 1 << 24, 1, 0, 'by_scene')
     items = mosaic_inputs(m, c['years'], c['k'][0], c['k'][1], c['mask'], c['seed'],
                           eng.device, bench.TARGET)
     params, _ = compile_params(c['line_cost'], c['rules'], c['mode'])
@@ -96,6 +103,9 @@ def main():
         print('oracle %d/%d px, differing values so far %d, %.0f s' % (
             b, end, sum(diff.values()), time.time() - t0), flush=True)
     res = {'config': args.config, 'labels_only': args.labels_only, 'pixels': P,
+           'bench_fields': args.bench_fields, 'whole_scene_launch': args.whole,
+           'kernel': 'lt_jit_analyze (JIT)' if runner.jit is not None else 'precompiled',
+           'deferred_pixels_last_launch': eng.last_deferred(),
            'checked': [args.first, end],
            'tile_pixels': m.tile, 'seed': c['seed'],
            'input': 'int16 bands + index_eqn "B1 - B2" (bench.py rank 0 scene, runner path)',

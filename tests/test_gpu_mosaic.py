@@ -37,14 +37,16 @@ def _same(a, b):
     return a == b
 
 
-def _bench_runner(cfg_name, fields, pixels=0):
+def _bench_runner(cfg_name, fields, pixels=0, whole=False):
+    """whole: the scene as ONE tile (one lt_analyze_tiles launch of 49 Mpx), as bench.py runs a
+    labels-only config on one GPU (bench.py main: `whole`); else 16.8 Mpx tiles."""
     c = bench.CONFIGS[cfg_name]
     P = pixels or c['pixels']
     if 'scenes' in c:
         tile = ((P + 7) // 8 + 63) // 64 * 64
         m = Mosaic([P] * c['scenes'], tile, 1, 0, 'round_robin')
     else:
-        m = Mosaic([P], 1 << 24, 1, 0, 'by_scene')
+        m = Mosaic([P], P if whole else 1 << 24, 1, 0, 'by_scene')
     eng = get_engine(0)
     items = mosaic_inputs(m, c['years'], c['k'][0], c['k'][1], c['mask'], c['seed'],
                           eng.device, bench.TARGET)
@@ -53,15 +55,20 @@ def _bench_runner(cfg_name, fields, pixels=0):
     return MosaicRunner(eng, m, params, items, fields, fn), params
 
 
-@pytest.mark.parametrize('cfg', ['c2', 'c3', 'c4', 'c5', 'c2-bench', 'c3-bench'])
+@pytest.mark.parametrize('cfg', ['c2', 'c3', 'c4', 'c5', 'c2-bench', 'c3-bench',
+                                 'c2-bench-whole', 'c3-bench-whole'])
 def test_bench_path_full_size_sampled_vs_oracle(cfg):
     """'c2' / 'c3' add the val_fit / vertex planes (the emulated-fit, year-major output path);
     'c2-bench' / 'c3-bench' request exactly bench.py's fields (labels only), so the kernel
     instance bench.py times runs: the certified labels path (lt_fast.h LT_CERT_RULES) over an
     int16 series with the fused 'B1 - B2' load stage, 1 rule (c2) or 3 rules with onset / duration
-    / pre_threshold filters over mask bit planes (c3), on one full 16.8 Mpx tile each."""
+    / pre_threshold filters over mask bit planes (c3), on one full 16.8 Mpx tile each.
+    '-bench-whole': the exact launch bench.py times on one GPU — the whole 49 Mpx scene as one
+    tile, so one analyze launch of 765,625 waves, one deferred list sized for 49 Mpx and one
+    resolve launch (bench.py main, `whole`)."""
     from oracle import oracle
-    bench_fields = cfg.endswith('-bench')
+    bench_fields = '-bench' in cfg
+    whole = cfg.endswith('-whole')
     cfg = cfg.split('-')[0]
     c = bench.CONFIGS[cfg]
     fields = ['status', 'matched', 'class_val', 'onset_year', 'duration', 'magnitude']
@@ -69,7 +76,10 @@ def test_bench_path_full_size_sampled_vs_oracle(cfg):
         fields += bench.TRENDLINE_FIELDS
     elif cfg != 'c4' and not bench_fields:
         fields += ['val_fit', 'vertex']
-    runner, params = _bench_runner(cfg, fields)
+    runner, params = _bench_runner(cfg, fields, whole=whole)
+    if whole:  # the geometry bench.py times: one tile, one launch
+        assert len(runner.items) == 1 and runner.items[0].tile.n == bench.CONFIGS[cfg]['pixels']
+        assert runner.jit is not None  # the JIT kernels specialised for this launch
     runner.step()
     torch.cuda.synchronize()
     m = runner.m

@@ -31,14 +31,33 @@
     }                                                                         \
   } while (0)
 
+// Round-5 kinds (the forms the compiler emits most in the c2 kernel):
+//   cndmask_b32_vcc       e32 selects on VCC, VCC written by an s_mov_b64 each iteration (round 4:
+//                         22.9 cycles at every occupancy, unexplained)
+//   cndmask_vcc_valu      e32 selects on VCC, VCC written ONCE per iteration by a VOPC e32 compare
+//   cmp_cndmask_vcc       the compiler's pair: v_cmp_*_e32 (VCC) then v_cndmask_b32_e32, eight
+//                         independent pairs per block (one VCC: each pair waits on its compare)
+//   cndmask_e64_vcc       e64 selects naming vcc as the mask, VCC written by s_mov each iteration
+//   cndmask_e64_smov      e64 selects on an SGPR pair written by s_mov each iteration (is it the
+//                         SALU write of a mask, or VCC itself?)
+//   cndmask_e64_vcmp      e64 selects on an SGPR pair written by a VOPC e64 compare each iteration
+//   mov_b64               v_mov_b64 (gfx950's 64-bit move)
+//   cmp_e32               VOPC e32 compares writing VCC (back to back)
+//   nop_mix               one s_nop 0 per eight v_add_u32 (the hazard padding the compiler emits)
 enum Kind { ADD_U32, CNDMASK, CMP, FMA_F32, FMA_F32K, ADD_F64, FMA_F64, MUL_F64, RCP_F64, LSHL_B64,
-            MIX_C2, MOV_B32, CNDMASK_VCC, NKIND };
+            MIX_C2, MOV_B32, CNDMASK_VCC, CNDMASK_VCC_VALU, CMP_CNDMASK_VCC, CNDMASK_E64_VCC,
+            CNDMASK_E64_SMOV, CNDMASK_E64_VCMP, MOV_B64, CMP_E32, NOP_MIX, NKIND };
 static const char* kKindName[NKIND] = {"add_u32", "cndmask_b32", "cmp_gt_u32", "fma_f32",
                                        "fma_f32_k", "add_f64", "fma_f64", "mul_f64", "rcp_f64",
-                                       "lshlrev_b64", "mix_c2", "mov_b32", "cndmask_b32_vcc"};
+                                       "lshlrev_b64", "mix_c2", "mov_b32", "cndmask_b32_vcc",
+                                       "cndmask_vcc_valu", "cmp_cndmask_vcc", "cndmask_e64_vcc",
+                                       "cndmask_e64_smov", "cndmask_e64_vcmp", "mov_b64",
+                                       "cmp_e32", "nop_mix"};
 // VALU / SALU instructions per loop iteration of each kind (the asm blocks below)
-static const int kValuPerIter[NKIND] = {64, 64, 64, 64, 64, 64, 64, 64, 32, 64, 103, 64, 64};
-static const int kSaluPerIter[NKIND] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 50, 0, 1};
+static const int kValuPerIter[NKIND] = {64, 64, 64, 64, 64, 64, 64, 64, 32, 64, 103, 64, 64,
+                                        65, 64, 64, 64, 65, 64, 64, 64};
+static const int kSaluPerIter[NKIND] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 50, 0, 1,
+                                        0, 0, 1, 1, 0, 0, 0, 8};
 
 #define R8(s) s s s s s s s s
 
@@ -99,6 +118,74 @@ __global__ void __launch_bounds__(64) valu_kernel(unsigned* out, unsigned long l
                    : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)
                    : "v"(inc), "s"(sel)
                    : "vcc");
+    } else if constexpr (K == CNDMASK_VCC_VALU) {  // VCC from one VOPC e32 compare per iteration
+      asm volatile("v_cmp_gt_u32_e32 vcc, %8, %9\n"
+                   R8("v_cndmask_b32_e32 %0, %0, %8, vcc\n v_cndmask_b32_e32 %1, %1, %8, vcc\n"
+                      "v_cndmask_b32_e32 %2, %2, %8, vcc\n v_cndmask_b32_e32 %3, %3, %8, vcc\n"
+                      "v_cndmask_b32_e32 %4, %4, %8, vcc\n v_cndmask_b32_e32 %5, %5, %8, vcc\n"
+                      "v_cndmask_b32_e32 %6, %6, %8, vcc\n v_cndmask_b32_e32 %7, %7, %8, vcc\n")
+                   : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)
+                   : "v"(inc), "v"(t)
+                   : "vcc");
+    } else if constexpr (K == CMP_CNDMASK_VCC) {  // compare (VCC) -> select pairs, eight chains
+#define CC8 "v_cmp_gt_u32_e32 vcc, %8, %0\n v_cndmask_b32_e32 %0, %0, %8, vcc\n" \
+            "v_cmp_gt_u32_e32 vcc, %8, %1\n v_cndmask_b32_e32 %1, %1, %8, vcc\n" \
+            "v_cmp_gt_u32_e32 vcc, %8, %2\n v_cndmask_b32_e32 %2, %2, %8, vcc\n" \
+            "v_cmp_gt_u32_e32 vcc, %8, %3\n v_cndmask_b32_e32 %3, %3, %8, vcc\n" \
+            "v_cmp_gt_u32_e32 vcc, %8, %4\n v_cndmask_b32_e32 %4, %4, %8, vcc\n" \
+            "v_cmp_gt_u32_e32 vcc, %8, %5\n v_cndmask_b32_e32 %5, %5, %8, vcc\n" \
+            "v_cmp_gt_u32_e32 vcc, %8, %6\n v_cndmask_b32_e32 %6, %6, %8, vcc\n" \
+            "v_cmp_gt_u32_e32 vcc, %8, %7\n v_cndmask_b32_e32 %7, %7, %8, vcc\n"
+      asm volatile(CC8 CC8 CC8 CC8
+                   : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)
+                   : "v"(inc)
+                   : "vcc");
+#undef CC8
+    } else if constexpr (K == CNDMASK_E64_VCC) {  // e64 selects naming vcc, VCC from s_mov
+      asm volatile("s_mov_b64 vcc, %9\n"
+                   R8("v_cndmask_b32_e64 %0, %0, %8, vcc\n v_cndmask_b32_e64 %1, %1, %8, vcc\n"
+                      "v_cndmask_b32_e64 %2, %2, %8, vcc\n v_cndmask_b32_e64 %3, %3, %8, vcc\n"
+                      "v_cndmask_b32_e64 %4, %4, %8, vcc\n v_cndmask_b32_e64 %5, %5, %8, vcc\n"
+                      "v_cndmask_b32_e64 %6, %6, %8, vcc\n v_cndmask_b32_e64 %7, %7, %8, vcc\n")
+                   : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)
+                   : "v"(inc), "s"(sel)
+                   : "vcc");
+    } else if constexpr (K == CNDMASK_E64_SMOV) {  // e64 selects on an SGPR pair from s_mov
+      asm volatile("s_mov_b64 %8, %10\n"
+                   R8("v_cndmask_b32_e64 %0, %0, %9, %8\n v_cndmask_b32_e64 %1, %1, %9, %8\n"
+                      "v_cndmask_b32_e64 %2, %2, %9, %8\n v_cndmask_b32_e64 %3, %3, %9, %8\n"
+                      "v_cndmask_b32_e64 %4, %4, %9, %8\n v_cndmask_b32_e64 %5, %5, %9, %8\n"
+                      "v_cndmask_b32_e64 %6, %6, %9, %8\n v_cndmask_b32_e64 %7, %7, %9, %8\n")
+                   : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7),
+                     "+s"(m0)
+                   : "v"(inc), "s"(sel));
+    } else if constexpr (K == CNDMASK_E64_VCMP) {  // e64 selects on an SGPR pair from a VOPC e64
+      asm volatile("v_cmp_gt_u32_e64 %8, %9, %10\n"
+                   R8("v_cndmask_b32_e64 %0, %0, %9, %8\n v_cndmask_b32_e64 %1, %1, %9, %8\n"
+                      "v_cndmask_b32_e64 %2, %2, %9, %8\n v_cndmask_b32_e64 %3, %3, %9, %8\n"
+                      "v_cndmask_b32_e64 %4, %4, %9, %8\n v_cndmask_b32_e64 %5, %5, %9, %8\n"
+                      "v_cndmask_b32_e64 %6, %6, %9, %8\n v_cndmask_b32_e64 %7, %7, %9, %8\n")
+                   : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7),
+                     "+s"(m0)
+                   : "v"(inc), "v"(t));
+    } else if constexpr (K == MOV_B64) {  // 64-bit moves (a rotation of eight register pairs)
+      asm volatile(R8("v_mov_b64 %0, %1\n v_mov_b64 %1, %2\n v_mov_b64 %2, %3\n v_mov_b64 %3, %4\n"
+                      "v_mov_b64 %4, %5\n v_mov_b64 %5, %6\n v_mov_b64 %6, %7\n v_mov_b64 %7, %0\n")
+                   : "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3), "+v"(q4), "+v"(q5), "+v"(q6), "+v"(q7));
+    } else if constexpr (K == CMP_E32) {  // VOPC e32 compares writing VCC, back to back
+      asm volatile(R8("v_cmp_gt_u32_e32 vcc, %8, %0\n v_cmp_gt_u32_e32 vcc, %8, %1\n"
+                      "v_cmp_gt_u32_e32 vcc, %8, %2\n v_cmp_gt_u32_e32 vcc, %8, %3\n"
+                      "v_cmp_gt_u32_e32 vcc, %8, %4\n v_cmp_gt_u32_e32 vcc, %8, %5\n"
+                      "v_cmp_gt_u32_e32 vcc, %8, %6\n v_cmp_gt_u32_e32 vcc, %8, %7\n")
+                   : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)
+                   : "v"(inc)
+                   : "vcc");
+    } else if constexpr (K == NOP_MIX) {  // an s_nop 0 after every eight 32-bit adds
+      asm volatile(R8("v_add_u32 %0, %0, %8\n v_add_u32 %1, %1, %8\n v_add_u32 %2, %2, %8\n v_add_u32 %3, %3, %8\n"
+                      "v_add_u32 %4, %4, %8\n v_add_u32 %5, %5, %8\n v_add_u32 %6, %6, %8\n v_add_u32 %7, %7, %8\n"
+                      "s_nop 0\n")
+                   : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)
+                   : "v"(inc));
     } else if constexpr (K == FMA_F32K) {  // two VGPR sources and an inline constant
       asm volatile(R8("v_fma_f32 %0, %0, %8, 0.5\n v_fma_f32 %1, %1, %8, 0.5\n v_fma_f32 %2, %2, %8, 0.5\n"
                       "v_fma_f32 %3, %3, %8, 0.5\n v_fma_f32 %4, %4, %8, 0.5\n v_fma_f32 %5, %5, %8, 0.5\n"
@@ -197,6 +284,14 @@ static KFn kernel_of(int k) {
     case RCP_F64: return valu_kernel<RCP_F64>;
     case LSHL_B64: return valu_kernel<LSHL_B64>;
     case MIX_C2: return valu_kernel<MIX_C2>;
+    case CNDMASK_VCC_VALU: return valu_kernel<CNDMASK_VCC_VALU>;
+    case CMP_CNDMASK_VCC: return valu_kernel<CMP_CNDMASK_VCC>;
+    case CNDMASK_E64_VCC: return valu_kernel<CNDMASK_E64_VCC>;
+    case CNDMASK_E64_SMOV: return valu_kernel<CNDMASK_E64_SMOV>;
+    case CNDMASK_E64_VCMP: return valu_kernel<CNDMASK_E64_VCMP>;
+    case MOV_B64: return valu_kernel<MOV_B64>;
+    case CMP_E32: return valu_kernel<CMP_E32>;
+    case NOP_MIX: return valu_kernel<NOP_MIX>;
     default: return valu_kernel<MIX_C2>;
   }
 }
@@ -225,7 +320,11 @@ int main(int argc, char** argv) {
          "\"iters\": %d, \"generations\": %d, \"results\": [",
          prop.name, prop.gcnArchName, cus, simds, prop.clockRate, iters, gens);
   bool first = true;
+  // argv[2]: a comma-separated list of kinds to run (default: all)
+  const std::string only = argc > 2 ? std::string(",") + argv[2] + "," : "";
   for (int k = 0; k < NKIND; k++) {
+    if (!only.empty() && only.find(std::string(",") + kKindName[k] + ",") == std::string::npos)
+      continue;
     KFn fn = kernel_of(k);
     for (int w : wps) {
       const size_t lds = lds_cu / (4 * w) - 256;  // <= 4 W one-wave workgroups per CU
