@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define LT_ABI_VERSION 6
+#define LT_ABI_VERSION 7
 #define LT_MAX_YEARS 64   /* distinct calendar years per scene (T <= 40 in every config) */
 #define LT_MAX_OBS 1024   /* observations per scene (K*T) */
 #define LT_MAX_RULES 16
@@ -345,6 +345,43 @@ int lt_index_apply(lt_ctx* ctx, const lt_index* fn, const lt_index_io* io, void*
  * terms, mixed integer node types, a band type the kernel does not read, more than
  * LT_LIN_MAX_BANDS bands): such programs keep lt_index_apply. Host only, no context. */
 int lt_index_linearize(const lt_index_prog* prog, lt_index_lin* out);
+
+/* ---- JIT kernels (lt_tile_in.index; ABI 7) -------------------------------------------------------
+ * A tile carrying an index_eqn program runs analyze / resolve kernels compiled for it (hiprtc,
+ * lt_jit.h) from kernel headers embedded in this library. Until a tile's module is ready, or if its
+ * compile fails, the tile runs on the precompiled kernels instead — a linear program through its
+ * lt_index_lin form, any other through its index raster (the program's load kernel into a context
+ * scratch buffer) — with the same results; lt_ctx_jit_stats counts both kinds of tile. */
+enum { LT_JIT_SYNC = 0,    /* a launch needing a module compiles it first (the default)        */
+       LT_JIT_ASYNC = 1 }; /* modules compile on worker threads; tiles launched before theirs
+                              is ready take the precompiled kernels                             */
+int lt_ctx_set_jit_mode(lt_ctx* ctx, int32_t mode);
+/* Compile (wait != 0) or start compiling (wait == 0, on a worker thread) the module a
+ * lt_analyze_tiles call with this scene, params, tile and output set would use, so that no launch
+ * waits for hiprtc (e.g. every scene of a mosaic before the first tile). LT_OK also when `in`
+ * carries no program; LT_ERR_JIT (the log in lt_last_error) when a waited-for compile failed. */
+int lt_jit_prepare(lt_ctx* ctx, const lt_scene* scene, const lt_params* params,
+                   const lt_tile_in* in, const lt_tile_out* out, int32_t wait);
+typedef struct {
+  int64_t jit_tiles;       /* tiles launched on JIT kernels                                    */
+  int64_t fallback_tiles;  /* tiles with a program launched on the precompiled kernels         */
+  int64_t compiles;        /* modules compiled with hiprtc                                     */
+  int64_t disk_hits;       /* modules read from the disk cache (LT_JIT_CACHE)                  */
+  int64_t failures;        /* modules whose compile or load failed                             */
+  int64_t modules;         /* modules loaded now (least recently used unloaded past a cap)     */
+  int64_t evictions;       /* modules unloaded                                                 */
+  int64_t pending;         /* compiles still running                                           */
+} lt_jit_stats;
+/* The context's JIT counters since creation and the last JIT failure message (NUL-terminated into
+ * last_error, at most cap bytes; may be NULL). Loads modules whose compile has finished. */
+int lt_ctx_jit_stats(lt_ctx* ctx, lt_jit_stats* out, char* last_error, int64_t cap);
+/* The module source the context would compile for a tile of this scene and params carrying
+ * `prog` (masked: the tile has a cloud mask; year_out: a per-year plane is requested), with the
+ * launch constants (LT_JIT_SRC_SPEC) and the scene's tables (LT_JIT_SRC_SCENE); host only, for
+ * inspection and ahead-of-time builds. Returns the length, or a negative LT_ERR_*. */
+enum { LT_JIT_SRC_SPEC = 1, LT_JIT_SRC_SCENE = 2 };
+int lt_jit_source(const lt_scene* scene, const lt_params* params, const lt_index_prog* prog,
+                  int32_t masked, int32_t year_out, int32_t flags, char* buf, int64_t cap);
 
 #ifdef __cplusplus
 }

@@ -10,7 +10,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, 'liblt_hip.so')
 
-LT_ABI_VERSION = 6
+LT_ABI_VERSION = 7
 LT_MAX_YEARS = 64
 LT_MAX_OBS = 1024
 LT_MAX_RULES = 16
@@ -171,7 +171,17 @@ EXPORTS = ['lt_abi_version', 'lt_ctx_create', 'lt_ctx_destroy', 'lt_last_error',
            'lt_analyze_tile', 'lt_analyze_tiles', 'lt_analyze_tiles_after', 'lt_label_tile', 'lt_ctx_set_timing', 'lt_ctx_stage_ms',
            'lt_ctx_last_deferred', 'lt_index_codegen', 'lt_index_compile', 'lt_index_apply',
            'lt_settings_compile', 'lt_raster_assemble', 'lt_winner_presence',
-           'lt_index_linearize']
+           'lt_index_linearize', 'lt_ctx_set_jit_mode', 'lt_jit_prepare', 'lt_ctx_jit_stats',
+           'lt_jit_source']
+
+LT_JIT_SYNC, LT_JIT_ASYNC = 0, 1
+LT_JIT_SRC_SPEC, LT_JIT_SRC_SCENE = 1, 2
+
+
+class LtJitStats(ctypes.Structure):
+    _fields_ = [(f, ctypes.c_int64) for f in ('jit_tiles', 'fallback_tiles', 'compiles',
+                                              'disk_hits', 'failures', 'modules', 'evictions',
+                                              'pending')]
 
 _LIB = None
 
@@ -220,6 +230,16 @@ def load_lib(path=None):
                                         ctypes.POINTER(LtSettings),
                                         ctypes.POINTER(ctypes.c_int32), ctypes.c_char_p,
                                         ctypes.c_int64]
+    lib.lt_ctx_set_jit_mode.argtypes = [vp, ctypes.c_int32]
+    lib.lt_jit_prepare.argtypes = [vp, ctypes.POINTER(LtScene), ctypes.POINTER(LtParams),
+                                   ctypes.POINTER(LtTileIn), ctypes.POINTER(LtTileOut),
+                                   ctypes.c_int32]
+    lib.lt_ctx_jit_stats.argtypes = [vp, ctypes.POINTER(LtJitStats), ctypes.c_char_p,
+                                     ctypes.c_int64]
+    lib.lt_jit_source.argtypes = [ctypes.POINTER(LtScene), ctypes.POINTER(LtParams),
+                                  ctypes.POINTER(LtIndexProg), ctypes.c_int32, ctypes.c_int32,
+                                  ctypes.c_int32, ctypes.c_char_p, ctypes.c_int64]
+    lib.lt_jit_source.restype = ctypes.c_int
     if lib.lt_abi_version() != LT_ABI_VERSION:
         raise RuntimeError('liblt_hip.so ABI %d != %d' % (lib.lt_abi_version(), LT_ABI_VERSION))
     if path is None:

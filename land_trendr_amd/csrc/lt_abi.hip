@@ -8,8 +8,11 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
 #include <map>
+#include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/lt_abi.h"
@@ -147,6 +150,24 @@ __global__ __launch_bounds__(kBlock) void raster_scatter_kernel(const lt_raster_
 
 }  // namespace
 
+// One JIT module of the context (lt_jit.h): compiled on the launching thread (LT_JIT_SYNC) or on
+// a worker (LT_JIT_ASYNC, lt_jit_prepare without wait), loaded on the launching thread once done.
+struct JitJob {
+  std::string src, arch, code, err;
+  bool ok = false, disk_hit = false;
+  std::atomic<bool> done{false};
+};
+struct JitEntry {
+  int state = 0;  // 0 compiling, 1 ready, -1 failed (its tiles take the precompiled kernels)
+  lt_jit_kernels k;
+  bool has_r64 = false, scene_spec = false;
+  std::string err;
+  std::shared_ptr<JitJob> job;
+  std::thread worker;
+  uint64_t last_use = 0;
+  hipEvent_t ev_last = nullptr;  // after the last resolve launch that used the module
+};
+
 struct lt_ctx {
   int device = 0;
   std::string err;
@@ -173,9 +194,18 @@ struct lt_ctx {
   bool set_used[kSets] = {};
   int last_set = 0, next_set = 0;
   std::map<std::string, lt_index*> index_fns;  // compiled load-stage kernels, by source
-  // JIT analyze / resolve kernels with an index_eqn program inlined (lt_jit.h), by program
-  // source and instance
-  std::map<std::string, lt_jit_kernels> jit;
+  // JIT analyze / resolve kernels with an index_eqn program inlined (lt_jit.h), by spec_key
+  std::map<uint64_t, JitEntry> jit;
+  int jit_mode = LT_JIT_SYNC;
+  uint64_t jit_clock = 0;      // launch counter for the modules' least-recently-used order
+  int jit_max_modules = 16;    // LT_JIT_MAX_MODULES
+  int jit_scene_max = 8;       // LT_JIT_SCENE_MAX: scene-specialised modules before the generic
+  lt_jit_stats jstats{};
+  std::string jit_err;         // the last JIT failure
+  std::string arch;            // the device's target id (hiprtc --offload-arch)
+  // the precompiled fallback of a non-linear program: its index raster per deferred-list set
+  void* d_iscratch[kSets] = {};
+  size_t iscratch_bytes[kSets] = {};
 };
 
 static int fail(lt_ctx* c, int code, const char* fmt, const char* detail = "") {
@@ -225,6 +255,11 @@ int lt_ctx_create(int device, lt_ctx** out) {
   *out = nullptr;
   lt_ctx* c = new lt_ctx();
   c->device = device;
+  // JIT module cache bounds (lt_abi.h LT_JIT_*; tests and long-running mosaics)
+  if (const char* e = getenv("LT_JIT_MAX_MODULES"))
+    if (atoi(e) >= 1) c->jit_max_modules = atoi(e);
+  if (const char* e = getenv("LT_JIT_SCENE_MAX"))
+    if (atoi(e) >= 0) c->jit_scene_max = atoi(e);
   hipError_t e = hipSetDevice(device);
   if (e == hipSuccess) e = hipHostMalloc((void**)&c->h_scene, sizeof(lt::DevScene));
   if (e == hipSuccess) e = hipMalloc((void**)&c->d_scene, sizeof(lt::DevScene));
@@ -263,8 +298,13 @@ int lt_ctx_destroy(lt_ctx* c) {
     if (c->ev_analyzed[s]) (void)hipEventDestroy(c->ev_analyzed[s]);
     if (c->ev_resolved[s]) (void)hipEventDestroy(c->ev_resolved[s]);
   }
-  for (auto& kv : c->jit)
-    if (kv.second.mod) (void)hipModuleUnload(kv.second.mod);
+  for (auto& kv : c->jit) {
+    if (kv.second.worker.joinable()) kv.second.worker.join();
+    if (kv.second.ev_last) (void)hipEventDestroy(kv.second.ev_last);
+    if (kv.second.k.mod) (void)hipModuleUnload(kv.second.k.mod);
+  }
+  for (int s = 0; s < lt_ctx::kSets; s++)
+    if (c->d_iscratch[s]) (void)hipFree(c->d_iscratch[s]);
   if (c->d_defer) (void)hipFree(c->d_defer);
   if (c->d_yflags) (void)hipFree(c->d_yflags);
   if (c->d_ndefer) (void)hipFree(c->d_ndefer);
@@ -343,18 +383,82 @@ static int check_tile(lt_ctx* c, const lt_tile_in* in, const lt_tile_out* out) {
   return LT_OK;
 }
 
+// the device's target id, for hiprtc (cached)
+static int device_arch(lt_ctx* c) {
+  if (!c->arch.empty()) return LT_OK;
+  hipDeviceProp_t prop;
+  HIP_OR_FAIL(c, hipGetDeviceProperties(&prop, c->device));
+  c->arch = prop.gcnArchName;
+  return LT_OK;
+}
+
+// Unload least-recently-used ready modules past the cap (LT_JIT_MAX_MODULES), never `keep`: a
+// module's last resolve launch is waited for first, so no queued kernel loses its code
+static void jit_evict(lt_ctx* c, uint64_t keep) {
+  for (;;) {
+    int ready = 0;
+    auto lru = c->jit.end();
+    for (auto it = c->jit.begin(); it != c->jit.end(); ++it) {
+      if (it->second.state != 1) continue;
+      ready++;
+      if (it->first != keep && (lru == c->jit.end() || it->second.last_use < lru->second.last_use))
+        lru = it;
+    }
+    if (ready <= c->jit_max_modules || lru == c->jit.end()) return;
+    JitEntry& e = lru->second;
+    if (e.ev_last) {
+      (void)hipEventSynchronize(e.ev_last);
+      (void)hipEventDestroy(e.ev_last);
+    }
+    if (e.k.mod) (void)hipModuleUnload(e.k.mod);
+    c->jit.erase(lru);
+    c->jstats.evictions++;
+  }
+}
+
+// A compiling entry whose job is done (or, when `wait`, once it is): join the worker, load the
+// module on this thread, count it
+static void jit_finish(lt_ctx* c, uint64_t key, JitEntry& e, bool wait) {
+  if (e.state != 0) return;
+  if (!e.job->done.load(std::memory_order_acquire)) {
+    if (!wait) return;
+    if (e.worker.joinable()) e.worker.join();
+  }
+  if (e.worker.joinable()) e.worker.join();
+  JitJob& j = *e.job;
+  std::string err = j.err;
+  bool ok = j.ok && lt_jit::load(j.code, e.has_r64, c->device, e.k, err);
+  if (ok) {
+    e.state = 1;
+    if (j.disk_hit) c->jstats.disk_hits++;
+    else c->jstats.compiles++;
+  } else {
+    e.state = -1;
+    e.err = err;
+    c->jit_err = err;
+    c->jstats.failures++;
+  }
+  e.job.reset();  // the code object's host copy
+  if (ok) jit_evict(c, key);
+}
+
 // The JIT analyze / resolve kernels of program f for a tile of Y year slots and n_rules rules
 // (lt_jit.h): the instance the product would dispatch to (MAXY, RMAX buckets, series type),
-// compiled on first use and cached in the context.
-static int jit_kernels(lt_ctx* c, const lt_index* f, int Y, const lt_params* prm,
+// specialised on the launch's uniform values unless LT_JIT_SPEC=0 and on the scene's tables
+// unless LT_JIT_SCENE=0 (or once the context holds LT_JIT_SCENE_MAX scene-specialised modules:
+// a mosaic of many scenes then shares one generic module per configuration). *entry is the ready
+// module, or NULL when it is still compiling (`wait` false) or failed: the tile then takes the
+// precompiled kernels (launch_tile). Errors are returned only for an invalid program or HIP.
+static int jit_acquire(lt_ctx* c, const lt_index* f, int Y, const lt_params* prm,
                        const lt_tile_in* in, const lt_tile_out* o, const lt::DevScene* scene,
-                       const lt_jit_kernels** out) {
+                       bool wait, JitEntry** entry, uint64_t* key_out = nullptr) {
+  *entry = nullptr;
   const int n_rules = prm->n_rules;
   const int maxy = Y <= 32 ? 32 : Y <= 48 ? 48 : 64;
   const int rmax = n_rules <= 1 ? 1 : n_rules <= 4 ? 4 : 16;
   const char* vt = lt_jit::series_type(f->out_type, n_rules);
-  // specialised on the launch's uniform values too (lt_jit.h Spec) unless LT_JIT_SPEC=0
   static const bool spec_on = !(getenv("LT_JIT_SPEC") && getenv("LT_JIT_SPEC")[0] == '0');
+  static const bool scene_on = !(getenv("LT_JIT_SCENE") && getenv("LT_JIT_SCENE")[0] == '0');
   lt_jit::Spec sp;
   if (spec_on) {
     sp.on = true;
@@ -363,23 +467,116 @@ static int jit_kernels(lt_ctx* c, const lt_index* f, int Y, const lt_params* prm
     sp.year_out = o->val_fit || o->fit_m || o->fit_b || o->right_m || o->right_b || o->spike ||
                   o->vertex;
     sp.params = *prm;
-    // the scene's tables too, unless LT_JIT_SCENE=0
-    static const bool scene_on = !(getenv("LT_JIT_SCENE") && getenv("LT_JIT_SCENE")[0] == '0');
     if (scene_on) sp.scene = scene;
   }
-  std::string err;
-  const std::string src = lt_jit::source(f->prog, maxy, rmax, vt, sp, err);
-  if (src.empty()) return fail(c, LT_ERR_ARG, "%s", err.c_str());
-  auto it = c->jit.find(src);
-  if (it == c->jit.end()) {
-    hipDeviceProp_t prop;
-    HIP_OR_FAIL(c, hipGetDeviceProperties(&prop, c->device));
-    lt_jit_kernels k;
-    if (!lt_jit::build(src, prop.gcnArchName, c->device, k, err))
-      return fail(c, LT_ERR_JIT, "%s", err.c_str());
-    it = c->jit.emplace(src, k).first;
+  uint64_t key = lt_jit::spec_key(f->prog, maxy, rmax, vt, sp);
+  auto it = c->jit.find(key);
+  if (it == c->jit.end() && sp.scene) {
+    int n_scene = 0;
+    for (auto& kv : c->jit) n_scene += kv.second.scene_spec ? 1 : 0;
+    if (n_scene >= c->jit_scene_max) {  // the generic-scene module of this configuration
+      sp.scene = nullptr;
+      key = lt_jit::spec_key(f->prog, maxy, rmax, vt, sp);
+      it = c->jit.find(key);
+    }
   }
-  *out = &it->second;
+  if (it == c->jit.end()) {
+    std::string err;
+    const std::string src = lt_jit::source(f->prog, maxy, rmax, vt, sp, err);
+    if (src.empty()) return fail(c, LT_ERR_ARG, "%s", err.c_str());
+    const int rc = device_arch(c);
+    if (rc != LT_OK) return rc;
+    it = c->jit.emplace(std::piecewise_construct, std::forward_as_tuple(key),
+                        std::forward_as_tuple()).first;
+    JitEntry& e = it->second;
+    e.has_r64 = strcmp(vt, "float") == 0;
+    e.scene_spec = sp.scene != nullptr;
+    e.job = std::make_shared<JitJob>();
+    e.job->src = src;
+    e.job->arch = c->arch;
+    auto run = [](std::shared_ptr<JitJob> j) {
+      j->ok = lt_jit::compile(j->src, j->arch, j->code, j->disk_hit, j->err);
+      j->done.store(true, std::memory_order_release);
+    };
+    if (wait) {
+      run(e.job);
+    } else {
+      try {
+        e.worker = std::thread(run, e.job);
+      } catch (...) {  // no thread: compile here
+        run(e.job);
+      }
+    }
+  }
+  JitEntry& e = it->second;
+  jit_finish(c, key, e, wait);
+  if (key_out) *key_out = key;
+  if (e.state == 1) {
+    e.last_use = ++c->jit_clock;
+    *entry = &e;
+  }
+  return LT_OK;
+}
+
+// The fused tile `in` (obs_bands + a program) as the precompiled kernels read it, when its JIT
+// kernels are not ready: a linear program as its lt_index_lin form (the precompiled fused load
+// stage), any other through its index raster, written into the context's scratch of deferred-list
+// set `set` by the program's load kernel on `stream` (lt_index_apply). false only on HIP errors.
+static int index_apply_impl(lt_ctx* c, const lt_index* f, const lt_index_io* io, hipStream_t st);
+static bool lin_tile_ok(const lt_tile_in& t, const lt_index_lin& L) {
+  if (L.n_bands < 1 || L.n_bands > LT_LIN_MAX_BANDS ||
+      (L.band_type != LT_T_I16 && L.band_type != LT_T_U16 && L.band_type != LT_T_U8 &&
+       L.band_type != LT_T_I32) ||
+      !lt_idx::is_int(L.wrap_type) || !lt_idx::ctype(L.out_type))
+    return false;
+  const bool planar = t.band_pix_stride == 1 && t.band_stride >= t.n_pix &&
+                      t.band_obs_stride >= (int64_t)L.n_bands * t.band_stride;
+  const bool interleaved = t.band_stride == 1 && t.band_pix_stride == L.n_bands &&
+                           t.band_obs_stride >= (int64_t)L.n_bands * t.n_pix;
+  if (!planar && !interleaved) return false;
+  const int64_t esz = (int64_t)lt_idx::type_size(L.band_type);
+  if (interleaved && L.n_bands == 2 && esz == 2 &&
+      ((uintptr_t)t.obs_bands % 4 != 0 || t.band_obs_stride % 2 != 0))
+    return false;
+  return true;
+}
+static int jit_fallback_tile(lt_ctx* c, const lt_tile_in* in, int n_obs, int set,
+                             hipStream_t stream, lt_tile_in& alt) {
+  alt = *in;
+  alt.index = nullptr;
+  const lt_index* f = in->index;
+  lt_index_lin lin;
+  if (lt_idx::linearize(f->prog, lin) && lin_tile_ok(alt, lin)) {
+    alt.lin = lin;
+    return LT_OK;
+  }
+  const size_t need = (size_t)n_obs * (size_t)in->stride * lt_idx::type_size(f->out_type);
+  if (c->iscratch_bytes[set] < need) {
+    if (c->d_iscratch[set]) {
+      HIP_OR_FAIL(c, hipStreamSynchronize(stream));
+      HIP_OR_FAIL(c, hipFree(c->d_iscratch[set]));
+    }
+    c->d_iscratch[set] = nullptr;
+    c->iscratch_bytes[set] = 0;
+    HIP_OR_FAIL(c, hipMalloc(&c->d_iscratch[set], need));
+    c->iscratch_bytes[set] = need;
+  }
+  lt_index_io io;
+  io.n_pix = in->n_pix;
+  io.n_obs = n_obs;
+  io.obs_stride = in->band_obs_stride;
+  io.band_stride = in->band_stride;
+  io.band_pix_stride = in->band_pix_stride;
+  io.out_stride = in->stride;  // the index raster shares the mask planes' row stride
+  io.bands = in->obs_bands;
+  io.out = c->d_iscratch[set];
+  if (n_obs > 0) {
+    const int rc = index_apply_impl(c, f, &io, stream);
+    if (rc != LT_OK) return rc;
+  }
+  alt.obs_bands = nullptr;
+  alt.obs_index = c->d_iscratch[set];
+  alt.index_type = f->out_type;
   return LT_OK;
 }
 
@@ -412,9 +609,21 @@ static int launch_tile(lt_ctx* c, const lt_params* prm, const lt_tile_in* in,
   if (nwave > 0x7fffffff) return fail(c, LT_ERR_LIMIT, "tile too large%s");
   lt::TileLaunch l{c->d_scene, prm, in, out, c->d_xtab, dl, dn, yf, Y, c->device, stream};
   const lt_jit_kernels* jk = nullptr;
+  JitEntry* je = nullptr;
+  lt_tile_in alt;  // the tile as the precompiled kernels read it (JIT kernels not ready)
   if (in->obs_bands && in->index) {  // a program inlined into JIT kernels (lt_jit.h)
-    const int rc = jit_kernels(c, in->index, Y, prm, in, out, c->h_scene, &jk);
+    const int rc = jit_acquire(c, in->index, Y, prm, in, out, c->h_scene,
+                               c->jit_mode == LT_JIT_SYNC, &je);
     if (rc != LT_OK) return rc;
+    if (je) {
+      jk = &je->k;
+      c->jstats.jit_tiles++;
+    } else {  // still compiling or failed: the precompiled kernels, same results
+      const int rf = jit_fallback_tile(c, in, c->h_scene->n_obs, set, stream, alt);
+      if (rf != LT_OK) return rf;
+      l.in = &alt;
+      c->jstats.fallback_tiles++;
+    }
   }
   // the JIT kernels' one argument, as the product kernels get it (lt_kernels.h kernel_args)
   auto jit_launch = [&](hipFunction_t f, unsigned grid, int64_t* list,
@@ -472,29 +681,20 @@ static int launch_tile(lt_ctx* c, const lt_params* prm, const lt_tile_in* in,
   HIP_OR_FAIL(c, hipGetLastError());
   if (ep[1]) HIP_OR_FAIL(c, hipEventRecord(ep[1]->stop, rstream));
   HIP_OR_FAIL(c, hipEventRecord(c->ev_resolved[set], rstream));
+  if (je) {  // the module may be unloaded (jit_evict) only after this launch
+    if (!je->ev_last)
+      HIP_OR_FAIL(c, hipEventCreateWithFlags(&je->ev_last, hipEventDisableTiming));
+    HIP_OR_FAIL(c, hipEventRecord(je->ev_last, rstream));
+  }
   c->last_set = set;
   c->launches++;
   return LT_OK;
 }
 
-int lt_analyze_tiles(lt_ctx* c, const lt_scene* sc, const lt_params* prm, int n_tiles,
-                     const lt_tile_in* ins, const lt_tile_out* outs, void* stream_) {
-  return lt_analyze_tiles_after(c, sc, prm, n_tiles, ins, outs, nullptr, stream_);
-}
-
-int lt_analyze_tiles_after(lt_ctx* c, const lt_scene* sc, const lt_params* prm, int n_tiles,
-                           const lt_tile_in* ins, const lt_tile_out* outs, void* const* ready,
-                           void* stream_) {
-  if (!c) return LT_ERR_ARG;
-  if (!sc || !prm || n_tiles < 0 || (n_tiles > 0 && (!ins || !outs)))
-    return fail(c, LT_ERR_ARG, "null argument%s");
-  int64_t cap = 0;
-  for (int t = 0; t < n_tiles; t++) {
-    const int rc = check_tile(c, &ins[t], &outs[t]);
-    if (rc != LT_OK) return rc;
-    cap = ins[t].n_pix > cap ? ins[t].n_pix : cap;
-  }
-  if (cap == 0) return LT_OK;
+// The scene's device table (lt_pixel.h DevScene), validated: scene metadata of lt_scene, the
+// rule count of prm, and the winner of every year when no observation is masked (pick_winners'
+// first observation, input order, at minimal |days|, as the kernels pick it)
+static int scene_from(lt_ctx* c, const lt_scene* sc, const lt_params* prm, lt::DevScene& tmp) {
   const int K = sc->n_obs, Y = sc->n_years;
   if (K < 0 || K > LT_MAX_OBS || Y < 0 || Y > LT_MAX_YEARS)
     return fail(c, LT_ERR_LIMIT, "scene exceeds LT_MAX_OBS/LT_MAX_YEARS%s");
@@ -517,11 +717,6 @@ int lt_analyze_tiles_after(lt_ctx* c, const lt_scene* sc, const lt_params* prm, 
   }
   if (Y > 0 && sc->year[Y - 1] - sc->year[0] > 255)
     return fail(c, LT_ERR_LIMIT, "year span above 255%s");
-  HIP_OR_FAIL(c, hipSetDevice(c->device));
-  hipStream_t stream = (hipStream_t)stream_;
-
-  // scene upload (skipped when identical to the resident one)
-  lt::DevScene tmp;
   memset(&tmp, 0, sizeof tmp);
   tmp.n_obs = K;
   tmp.n_years = Y;
@@ -543,6 +738,37 @@ int lt_analyze_tiles_after(lt_ctx* c, const lt_scene* sc, const lt_params* prm, 
       }
     tmp.winner_all[y] = best;
   }
+  return LT_OK;
+}
+
+int lt_analyze_tiles(lt_ctx* c, const lt_scene* sc, const lt_params* prm, int n_tiles,
+                     const lt_tile_in* ins, const lt_tile_out* outs, void* stream_) {
+  return lt_analyze_tiles_after(c, sc, prm, n_tiles, ins, outs, nullptr, stream_);
+}
+
+int lt_analyze_tiles_after(lt_ctx* c, const lt_scene* sc, const lt_params* prm, int n_tiles,
+                           const lt_tile_in* ins, const lt_tile_out* outs, void* const* ready,
+                           void* stream_) {
+  if (!c) return LT_ERR_ARG;
+  if (!sc || !prm || n_tiles < 0 || (n_tiles > 0 && (!ins || !outs)))
+    return fail(c, LT_ERR_ARG, "null argument%s");
+  int64_t cap = 0;
+  for (int t = 0; t < n_tiles; t++) {
+    const int rc = check_tile(c, &ins[t], &outs[t]);
+    if (rc != LT_OK) return rc;
+    cap = ins[t].n_pix > cap ? ins[t].n_pix : cap;
+  }
+  if (cap == 0) return LT_OK;
+  lt::DevScene tmp;
+  {
+    const int rc = scene_from(c, sc, prm, tmp);
+    if (rc != LT_OK) return rc;
+  }
+  const int Y = tmp.n_years;
+  HIP_OR_FAIL(c, hipSetDevice(c->device));
+  hipStream_t stream = (hipStream_t)stream_;
+
+  // scene upload (skipped when identical to the resident one)
   if (!c->scene_valid || memcmp(&tmp, c->h_scene, sizeof tmp) != 0) {
     // an earlier call, possibly on another stream, may still be reading d_scene: its last tile's
     // resolve (side stream, in order, after every analyze it waited for) marks the end of all of
@@ -715,6 +941,81 @@ int lt_label_tile(lt_ctx* c, const lt_label_in* in, const lt_params* prm, const 
   return LT_OK;
 }
 
+int lt_ctx_set_jit_mode(lt_ctx* c, int32_t mode) {
+  if (!c) return LT_ERR_ARG;
+  if (mode != LT_JIT_SYNC && mode != LT_JIT_ASYNC) return fail(c, LT_ERR_ARG, "bad JIT mode%s");
+  c->jit_mode = mode;
+  return LT_OK;
+}
+
+int lt_jit_prepare(lt_ctx* c, const lt_scene* sc, const lt_params* prm, const lt_tile_in* in,
+                   const lt_tile_out* out, int32_t wait) {
+  if (!c) return LT_ERR_ARG;
+  if (!sc || !prm || !in || !out) return fail(c, LT_ERR_ARG, "null argument%s");
+  if (!(in->obs_bands && in->index)) return LT_OK;  // no program: no JIT kernels
+  lt::DevScene tmp;
+  int rc = scene_from(c, sc, prm, tmp);
+  if (rc != LT_OK) return rc;
+  HIP_OR_FAIL(c, hipSetDevice(c->device));
+  JitEntry* e = nullptr;
+  uint64_t key = 0;
+  rc = jit_acquire(c, in->index, tmp.n_years, prm, in, out, &tmp, wait != 0, &e, &key);
+  if (rc != LT_OK) return rc;
+  auto it = c->jit.find(key);
+  if (it != c->jit.end() && it->second.state < 0)
+    return fail(c, LT_ERR_JIT, "%s", it->second.err.c_str());
+  return LT_OK;
+}
+
+int lt_ctx_jit_stats(lt_ctx* c, lt_jit_stats* out, char* last_error, int64_t cap) {
+  if (!c || !out) return LT_ERR_ARG;
+  // finish compiles that are done (the module is loaded on this thread)
+  for (auto& kv : c->jit)
+    if (kv.second.state == 0) jit_finish(c, kv.first, kv.second, false);
+  *out = c->jstats;
+  out->modules = 0;
+  out->pending = 0;
+  for (auto& kv : c->jit) {
+    out->modules += kv.second.state == 1 ? 1 : 0;
+    out->pending += kv.second.state == 0 ? 1 : 0;
+  }
+  if (last_error && cap > 0) {
+    const size_t n = c->jit_err.size() < (size_t)(cap - 1) ? c->jit_err.size() : (size_t)(cap - 1);
+    memcpy(last_error, c->jit_err.data(), n);
+    last_error[n] = 0;
+  }
+  return LT_OK;
+}
+
+int lt_jit_source(const lt_scene* sc, const lt_params* prm, const lt_index_prog* prog,
+                  int32_t masked, int32_t year_out, int32_t flags, char* buf, int64_t cap) {
+  if (!sc || !prm || !prog) return LT_ERR_ARG;
+  lt::DevScene tmp;
+  if (scene_from(nullptr, sc, prm, tmp) != LT_OK) return LT_ERR_ARG;
+  const int Y = tmp.n_years, n_rules = prm->n_rules;
+  const int maxy = Y <= 32 ? 32 : Y <= 48 ? 48 : 64;
+  const int rmax = n_rules <= 1 ? 1 : n_rules <= 4 ? 4 : 16;
+  lt_jit::Spec sp;
+  if (flags & LT_JIT_SRC_SPEC) {
+    sp.on = true;
+    sp.n_years = Y;
+    sp.masked = masked != 0;
+    sp.year_out = year_out != 0;
+    sp.params = *prm;
+    if (flags & LT_JIT_SRC_SCENE) sp.scene = &tmp;
+  }
+  std::string err;
+  const std::string src =
+      lt_jit::source(*prog, maxy, rmax, lt_jit::series_type(prog->out_type, n_rules), sp, err);
+  if (src.empty()) return LT_ERR_ARG;
+  if (buf && cap > 0) {
+    const size_t n = src.size() < (size_t)(cap - 1) ? src.size() : (size_t)(cap - 1);
+    memcpy(buf, src.data(), n);
+    buf[n] = 0;
+  }
+  return (int)src.size();
+}
+
 }  // extern "C"
 
 // ---- load stage (lt_index.h) ------------------------------------------------------------------
@@ -792,6 +1093,11 @@ int lt_index_linearize(const lt_index_prog* prog, lt_index_lin* out) {
 int lt_index_apply(lt_ctx* c, const lt_index* f, const lt_index_io* io, void* stream_) {
   if (!c) return LT_ERR_ARG;
   if (!f || !io) return fail(c, LT_ERR_ARG, "null argument%s");
+  return index_apply_impl(c, f, io, (hipStream_t)stream_);
+}
+
+static int index_apply_impl(lt_ctx* c, const lt_index* f, const lt_index_io* io,
+                            hipStream_t stream_) {
   if (io->n_pix < 0 || io->n_obs < 0 || io->n_obs > 65535) return fail(c, LT_ERR_ARG, "bad sizes%s");
   if (io->n_pix == 0 || io->n_obs == 0) return LT_OK;
   if (!io->bands || !io->out) return fail(c, LT_ERR_ARG, "null buffer%s");

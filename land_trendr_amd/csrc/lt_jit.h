@@ -11,11 +11,15 @@
 // hiprtc (LT_JIT_INDEX in lt_fast.h's winner pick). No index raster is written and no load kernel
 // runs between the analyze launches of consecutive tiles.
 //
-// One module per (program, MAXY, RMAX, series type), compiled on first use (~10 s per kernel)
-// and cached in the context; the code object is also cached on disk (LT_JIT_CACHE, default
-// <library dir>/../build/jit) under a hash of the generated source, the compile options and the
-// kernel headers it includes, so later processes load it at once.
+// One module per specialisation (program, MAXY, RMAX, series type, the launch constants of Spec),
+// compiled on first use (~10 s) or ahead of the launches (lt_jit_prepare), on the launching thread
+// or a worker (lt_ctx_set_jit_mode), and cached in the context (keyed by spec_key, least recently
+// used modules unloaded past a cap, lt_abi.hip); the code object is also cached on disk
+// (LT_JIT_CACHE, default <library dir>/../build/jit, at most kDiskCacheMax files) under a hash of
+// the generated source, the kernel headers (embedded in the library), the compile options, the
+// device's target id and the hiprtc / HIP runtime versions, so later processes load it at once.
 #pragma once
+#include <dirent.h>
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
@@ -25,6 +29,7 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -59,24 +64,20 @@ using __hip_internal::true_type;
 }
 )HIP";
 
-// the directory of the kernel headers: LT_SRC_DIR, else csrc/ beside this library
-inline std::string src_dir() {
-  const char* e = getenv("LT_SRC_DIR");
-  if (e && *e) return e;
-  Dl_info info;
-  if (dladdr((void*)&src_dir, &info) && info.dli_fname) {
-    std::string p = info.dli_fname;
-    const size_t s = p.rfind('/');
-    return (s == std::string::npos ? std::string(".") : p.substr(0, s)) + "/csrc";
-  }
-  return "csrc";
-}
+// The kernel headers the JIT kernels are compiled from, passed to hiprtc in memory under their bare
+// file names. By default the copies compiled into this library (build/gen/lt_jit_embed.inc,
+// written by __graft_entry__.embed_headers at build time): the JIT kernels then see exactly the
+// KernelArgs / lt_tile_in / lt_params layouts the library's host code was compiled with, and no
+// csrc/ tree is needed at run time. LT_SRC_DIR=<dir> (development only: header edits without a
+// rebuild) reads <dir>/lt_*.h and <dir>/../../include/lt_abi.h instead; a missing one is a JIT
+// failure, which the launch answers with the precompiled kernels (lt_abi.hip jit_fallback).
+#if __has_include("lt_jit_embed.inc")
+#include "lt_jit_embed.inc"
+#endif
 
-inline std::string cache_dir(const std::string& srcdir) {
-  const char* e = getenv("LT_JIT_CACHE");
-  if (e) return e;  // "" disables the disk cache
-  return srcdir + "/../../build/jit";
-}
+constexpr int kNHeaders = 5;
+constexpr const char* kHeaderName[kNHeaders] = {"lt_abi.h", "lt_lapack.h", "lt_pixel.h",
+                                                "lt_fast.h", "lt_kernels_dev.h"};
 
 inline bool read_file(const std::string& path, std::string& out) {
   FILE* f = fopen(path.c_str(), "rb");
@@ -89,12 +90,106 @@ inline bool read_file(const std::string& path, std::string& out) {
   return true;
 }
 
-inline uint64_t fnv1a(const std::string& s, uint64_t h = 1469598103934665603ull) {
-  for (unsigned char ch : s) {
-    h ^= ch;
+inline uint64_t fnv1a(const void* p, size_t n, uint64_t h = 1469598103934665603ull) {
+  const unsigned char* c = (const unsigned char*)p;
+  for (size_t i = 0; i < n; i++) {
+    h ^= c[i];
     h *= 1099511628211ull;
   }
   return h;
+}
+inline uint64_t fnv1a(const std::string& s, uint64_t h = 1469598103934665603ull) {
+  return fnv1a(s.data(), s.size(), h);
+}
+
+struct Headers {
+  std::vector<std::string> text;  // kNHeaders texts, in kHeaderName order
+  uint64_t hash = 0;
+  bool embedded = false;
+};
+
+// the headers (embedded, or LT_SRC_DIR's); false with err when one is missing
+inline bool headers(Headers& H, std::string& err) {
+  H.text.assign(kNHeaders, std::string());
+  const char* dir = getenv("LT_SRC_DIR");
+  if (!(dir && *dir)) {
+#ifdef LT_JIT_EMBEDDED
+    static_assert(kLtJitNHdr == kNHeaders, "embedded header list");
+    for (int i = 0; i < kNHeaders; i++) {
+      if (strcmp(kLtJitHdrName[i], kHeaderName[i]) != 0) {
+        err = "JIT: embedded header list out of order";
+        return false;
+      }
+      H.text[i] = kLtJitHdrText[i];
+    }
+    H.embedded = true;
+#else
+    // a library built without the embedded copies (a profiling variant): csrc/ beside it
+    Dl_info info;
+    static std::string lib_dir;
+    if (lib_dir.empty() && dladdr((void*)&headers, &info) && info.dli_fname) {
+      std::string p = info.dli_fname;
+      const size_t s = p.rfind('/');
+      lib_dir = (s == std::string::npos ? std::string(".") : p.substr(0, s)) + "/csrc";
+    }
+    dir = lib_dir.c_str();
+#endif
+  }
+  if (!H.embedded) {
+    const std::string d = dir;
+    for (int i = 0; i < kNHeaders; i++) {
+      const std::string path =
+          i == 0 ? d + "/../../include/lt_abi.h" : d + "/" + kHeaderName[i];
+      if (!read_file(path, H.text[i])) {
+        err = "JIT: kernel header " + path + " not found (LT_SRC_DIR)";
+        return false;
+      }
+      // the one relative include, as the embedded copies have it
+      const std::string rel = "#include \"../../include/lt_abi.h\"";
+      for (size_t at; (at = H.text[i].find(rel)) != std::string::npos;)
+        H.text[i].replace(at, rel.size(), "#include \"lt_abi.h\"");
+    }
+  }
+  uint64_t h = fnv1a(H.embedded ? "embedded" : "disk");
+  for (const std::string& t : H.text) h = fnv1a(t, h);
+  H.hash = h;
+  return true;
+}
+
+// the disk cache of code objects: LT_JIT_CACHE ("" disables it), else build/jit beside the
+// library's package directory
+inline std::string cache_dir() {
+  const char* e = getenv("LT_JIT_CACHE");
+  if (e) return e;
+  Dl_info info;
+  if (dladdr((void*)&cache_dir, &info) && info.dli_fname) {
+    std::string p = info.dli_fname;
+    const size_t s = p.rfind('/');
+    return (s == std::string::npos ? std::string(".") : p.substr(0, s)) + "/../build/jit";
+  }
+  return "build/jit";
+}
+
+// at most this many code objects stay in the disk cache (the oldest by mtime go first)
+constexpr int kDiskCacheMax = 64;
+
+inline void prune_disk_cache(const std::string& dir) {
+  DIR* d = opendir(dir.c_str());
+  if (!d) return;
+  std::vector<std::pair<double, std::string>> files;
+  while (dirent* e = readdir(d)) {
+    const std::string n = e->d_name;
+    if (n.compare(0, 7, "lt_jit_") != 0 || n.size() < 3 || n.substr(n.size() - 3) != ".co")
+      continue;
+    struct stat st;
+    const std::string path = dir + "/" + n;
+    if (stat(path.c_str(), &st) == 0)
+      files.emplace_back((double)st.st_mtim.tv_sec + 1e-9 * st.st_mtim.tv_nsec, path);
+  }
+  closedir(d);
+  if ((int)files.size() <= kDiskCacheMax) return;
+  std::sort(files.begin(), files.end());
+  for (size_t i = 0; i + kDiskCacheMax < files.size(); i++) remove(files[i].second.c_str());
 }
 
 // the series type of the analyze stage (lt_kernels.h series_kind): int16 for an int16 index,
@@ -141,6 +236,66 @@ inline std::string fmt_rule(const lt_rule& r) {
   return b;
 }
 
+// The environment switches that change the generated source (A/B runs: LT_JIT_DEFINES adds
+// compile-time switches, LT_JIT_WAVES the analyze kernel's occupancy): part of spec_key
+inline std::string env_switches() {
+  std::string r;
+  for (const char* v : {"LT_JIT_DEFINES", "LT_JIT_WAVES"}) {
+    const char* e = getenv(v);
+    r += std::string(v) + "=" + (e ? e : "") + ";";
+  }
+  return r;
+}
+
+// The identity of the module source() generates for these inputs, without generating it: the
+// context's module map is keyed on it (a tile launch hashes ~10 KB of scene tables instead of
+// formatting and comparing the whole source)
+inline uint64_t spec_key(const lt_index_prog& P, int maxy, int rmax, const char* vt,
+                         const Spec& sp) {
+  uint64_t h = fnv1a(&P.n_ops, sizeof P.n_ops);
+  h = fnv1a(&P.n_bands, sizeof P.n_bands, h);
+  h = fnv1a(&P.band_type, sizeof P.band_type, h);
+  h = fnv1a(&P.out_type, sizeof P.out_type, h);
+  for (int i = 0; i < P.n_ops && i < LT_MAX_PROG; i++) {
+    const lt_index_op& o = P.ops[i];
+    h = fnv1a(&o.op, sizeof o.op, h);
+    h = fnv1a(&o.type, sizeof o.type, h);
+    h = fnv1a(&o.ival, sizeof o.ival, h);
+    h = fnv1a(&o.fval, sizeof o.fval, h);
+  }
+  const int inst[3] = {maxy, rmax, (int)strlen(vt)};
+  h = fnv1a(inst, sizeof inst, fnv1a(vt, h));
+  const int flags[4] = {sp.on ? 1 : 0, sp.n_years, sp.masked ? 1 : 0, sp.year_out ? 1 : 0};
+  h = fnv1a(flags, sizeof flags, h);
+  if (sp.on) {
+    const lt_params& Q = sp.params;
+    h = fnv1a(&Q.line_cost, sizeof Q.line_cost, h);
+    h = fnv1a(&Q.n_rules, sizeof Q.n_rules, h);
+    h = fnv1a(&Q.pre_threshold_mode, sizeof Q.pre_threshold_mode, h);
+    for (int r = 0; r < Q.n_rules && r < LT_MAX_RULES; r++) {
+      const lt_rule& u = Q.rules[r];
+      const int32_t ints[5] = {u.change_type, u.onset_op, u.duration_op, u.pre_op, u.class_val};
+      const double dbl[3] = {u.onset_val, u.duration_val, u.pre_val};
+      h = fnv1a(dbl, sizeof dbl, fnv1a(ints, sizeof ints, h));
+    }
+  }
+  if (sp.on && sp.scene) {
+    const lt::DevScene& S = *sp.scene;
+    h = fnv1a(&S.n_obs, sizeof S.n_obs, h);
+    h = fnv1a(&S.n_years, sizeof S.n_years, h);
+    h = fnv1a(&S.feb29_mask, sizeof S.feb29_mask, h);
+    const int Y = S.n_years, K = S.n_obs;
+    h = fnv1a(S.year, sizeof(int32_t) * Y, h);
+    h = fnv1a(S.slot_begin, sizeof(int32_t) * (Y + 1), h);
+    h = fnv1a(S.order, sizeof(int32_t) * K, h);
+    h = fnv1a(S.dist, sizeof(int32_t) * K, h);
+    h = fnv1a(S.winner_all, sizeof(int32_t) * Y, h);
+  } else {
+    h = fnv1a("no-scene", h);
+  }
+  return fnv1a(env_switches(), h);
+}
+
 // The module source for program P, kernel instance (maxy, rmax), series type vt and
 // specialisation sp; "" with err
 inline std::string source(const lt_index_prog& P, int maxy, int rmax, const char* vt,
@@ -172,7 +327,7 @@ inline std::string source(const lt_index_prog& P, int maxy, int rmax, const char
     const lt_params& Q = sp.params;
     char d[512];
     snprintf(d, sizeof d,
-             "#include \"../../include/lt_abi.h\"\n#define LT_SPEC_Y %d\n#define LT_SPEC_MASKED %d\n"
+             "#include \"lt_abi.h\"\n#define LT_SPEC_Y %d\n#define LT_SPEC_MASKED %d\n"
              "#define LT_SPEC_YEAR_OUT %d\n#define LT_SPEC_NRULES %d\n#define LT_SPEC_PRE_MODE %d\n"
              "#define LT_SPEC_LINE_COST %a\n",
              sp.n_years, sp.masked ? 1 : 0, sp.year_out ? 1 : 0, Q.n_rules, Q.pre_threshold_mode,
@@ -220,82 +375,104 @@ inline std::string source(const lt_index_prog& P, int maxy, int rmax, const char
   return src;
 }
 
-// compile (or load from the disk cache) and load the module; false with err set
-inline bool build(const std::string& src, const std::string& arch, int device,
-                  lt_jit_kernels& out, std::string& err) {
-  const std::string dir = src_dir();
-  const std::string arch_opt = "--offload-arch=" + arch;  // the device's full target id
-  const std::string inc_opt = "-I" + dir;
-  std::vector<const char*> opts = {arch_opt.c_str(), "-O3", "-ffp-contract=off", "-std=c++17",
-                                   inc_opt.c_str()};
-  // cache key: the source, the options and every kernel header the source includes
-  uint64_t h = fnv1a(src);
-  for (const char* o : opts) h = fnv1a(o, h);
-  for (const char* f : {"lt_kernels_dev.h", "lt_fast.h", "lt_pixel.h", "lt_lapack.h"}) {
-    std::string text;
-    if (!read_file(dir + "/" + f, text)) {
-      err = "JIT: kernel header " + dir + "/" + f + " not found (LT_SRC_DIR)";
-      return false;
-    }
-    h = fnv1a(text, h);
-  }
-  {
-    std::string text;
-    if (read_file(dir + "/../../include/lt_abi.h", text)) h = fnv1a(text, h);
-  }
-  const std::string cdir = cache_dir(dir);
+// The identity of everything a module's code depends on besides its source: the kernel headers,
+// the compile options, the hiprtc and HIP runtime versions (the device's target id is one of the
+// options). The disk cache's file name is its hash with the source's.
+inline uint64_t env_key(const Headers& H, const std::vector<std::string>& opts) {
+  uint64_t h = H.hash;
+  for (const std::string& o : opts) h = fnv1a(o, h);
+  int maj = 0, min = 0, rt = 0;
+  (void)hiprtcVersion(&maj, &min);
+  (void)hipRuntimeGetVersion(&rt);
+  const int v[3] = {maj, min, rt};
+  return fnv1a(v, sizeof v, h);
+}
+
+inline std::vector<std::string> options(const std::string& arch) {
+  return {"--offload-arch=" + arch, "-O3", "-ffp-contract=off", "-std=c++17"};
+}
+
+// Compile `src` for `arch` into a code object (or read it from the disk cache). Host work only —
+// hiprtc and file IO, no HIP runtime call that touches the device — so it may run on a worker
+// thread (lt_abi.hip LT_JIT_ASYNC). false with err set.
+inline bool compile(const std::string& src, const std::string& arch, std::string& code,
+                    bool& disk_hit, std::string& err) {
+  disk_hit = false;
+  Headers H;
+  if (!headers(H, err)) return false;
+  const std::vector<std::string> opts = options(arch);
+  const uint64_t h = fnv1a(src, env_key(H, opts));
+  const std::string cdir = cache_dir();
   char name[64];
   snprintf(name, sizeof name, "/lt_jit_%016llx.co", (unsigned long long)h);
   const std::string cpath = cdir.empty() ? "" : cdir + name;
-  std::string code;
-  if (cpath.empty() || !read_file(cpath, code) || code.empty()) {
-    hiprtcProgram rp;
-    if (hiprtcCreateProgram(&rp, src.c_str(), "lt_jit.hip", 0, nullptr, nullptr) !=
-        HIPRTC_SUCCESS) {
-      err = "hiprtcCreateProgram failed";
-      return false;
-    }
-    const hiprtcResult rc = hiprtcCompileProgram(rp, (int)opts.size(), opts.data());
-    if (rc != HIPRTC_SUCCESS) {
-      size_t n = 0;
-      hiprtcGetProgramLogSize(rp, &n);
-      std::string log(n, '\0');
-      if (n) hiprtcGetProgramLog(rp, &log[0]);
-      hiprtcDestroyProgram(&rp);
-      err = "hiprtc (JIT analyze kernel): " + log.substr(0, 2000);
-      return false;
-    }
-    size_t code_size = 0;
-    hiprtcGetCodeSize(rp, &code_size);
-    code.assign(code_size, '\0');
-    hiprtcGetCode(rp, &code[0]);
-    hiprtcDestroyProgram(&rp);
-    if (!cpath.empty()) {  // best effort: a cache that cannot be written is skipped
-      for (size_t i = 1; i <= cdir.size(); i++)  // mkdir -p
-        if (i == cdir.size() || cdir[i] == '/') mkdir(cdir.substr(0, i).c_str(), 0755);
-      const std::string tmp = cpath + "." + std::to_string((long long)getpid());
-      FILE* f = fopen(tmp.c_str(), "wb");
-      if (f) {
-        const bool ok = fwrite(code.data(), 1, code.size(), f) == code.size();
-        fclose(f);
-        if (!ok || rename(tmp.c_str(), cpath.c_str()) != 0) remove(tmp.c_str());
-      }
-    }
+  if (!cpath.empty() && read_file(cpath, code) && !code.empty()) {
+    disk_hit = true;
+    return true;
   }
+  std::vector<const char*> hdr_text, hdr_name;
+  for (int i = 0; i < kNHeaders; i++) {
+    hdr_text.push_back(H.text[i].c_str());
+    hdr_name.push_back(kHeaderName[i]);
+  }
+  hiprtcProgram rp;
+  if (hiprtcCreateProgram(&rp, src.c_str(), "lt_jit.hip", kNHeaders, hdr_text.data(),
+                          hdr_name.data()) != HIPRTC_SUCCESS) {
+    err = "hiprtcCreateProgram failed";
+    return false;
+  }
+  std::vector<const char*> o;
+  for (const std::string& s : opts) o.push_back(s.c_str());
+  const hiprtcResult rc = hiprtcCompileProgram(rp, (int)o.size(), o.data());
+  if (rc != HIPRTC_SUCCESS) {
+    size_t n = 0;
+    hiprtcGetProgramLogSize(rp, &n);
+    std::string log(n, '\0');
+    if (n) hiprtcGetProgramLog(rp, &log[0]);
+    hiprtcDestroyProgram(&rp);
+    err = "hiprtc (JIT analyze kernel): " + log.substr(0, 2000);
+    return false;
+  }
+  size_t code_size = 0;
+  hiprtcGetCodeSize(rp, &code_size);
+  code.assign(code_size, '\0');
+  hiprtcGetCode(rp, &code[0]);
+  hiprtcDestroyProgram(&rp);
+  if (!cpath.empty()) {  // best effort: a cache that cannot be written is skipped
+    for (size_t i = 1; i <= cdir.size(); i++)  // mkdir -p
+      if (i == cdir.size() || cdir[i] == '/') mkdir(cdir.substr(0, i).c_str(), 0755);
+    const std::string tmp = cpath + "." + std::to_string((long long)getpid()) + "." +
+                            std::to_string((unsigned long long)(uintptr_t)&code);
+    FILE* f = fopen(tmp.c_str(), "wb");
+    if (f) {
+      const bool ok = fwrite(code.data(), 1, code.size(), f) == code.size();
+      fclose(f);
+      if (!ok || rename(tmp.c_str(), cpath.c_str()) != 0) remove(tmp.c_str());
+    }
+    prune_disk_cache(cdir);
+  }
+  return true;
+}
+
+// load a code object as a module on the calling thread's device; false with err set
+inline bool load(const std::string& code, bool has_resolve64, int device, lt_jit_kernels& out,
+                 std::string& err) {
   if (hipModuleLoadData(&out.mod, code.data()) != hipSuccess ||
       hipModuleGetFunction(&out.analyze, out.mod, "lt_jit_analyze") != hipSuccess ||
       hipModuleGetFunction(&out.resolve, out.mod, "lt_jit_resolve") != hipSuccess) {
     if (out.mod) (void)hipModuleUnload(out.mod);
     out = lt_jit_kernels{};
+    (void)hipGetLastError();
     err = "JIT module load failed";
     return false;
   }
   // (a binary64 resolve exists for the non-int16 series types only: a failed lookup would leave
   // "named symbol not found" as HIP's last error for the next launch check to find)
-  if (src.find("lt_jit_resolve64") != std::string::npos &&
+  if (has_resolve64 &&
       hipModuleGetFunction(&out.resolve64, out.mod, "lt_jit_resolve64") != hipSuccess) {
     (void)hipModuleUnload(out.mod);
     out = lt_jit_kernels{};
+    (void)hipGetLastError();
     err = "JIT module load failed (lt_jit_resolve64)";
     return false;
   }

@@ -264,6 +264,40 @@ class Engine:
                                                 ctypes.c_void_p(st.cuda_stream)),
                     'lt_raster_assemble')
 
+    # --- JIT kernels of tiles carrying a program (lt_jit.h; lt_ctx_set_jit_mode, lt_jit_prepare) ---
+    def set_jit_mode(self, asynchronous):
+        """False (default): a launch needing a JIT module compiles it first. True: modules compile
+        on worker threads and tiles launched before theirs is ready run on the precompiled kernels
+        (same results; counted in jit_stats()['fallback_tiles'])."""
+        self._check(self.lib.lt_ctx_set_jit_mode(
+            self.ctx, _abi.LT_JIT_ASYNC if asynchronous else _abi.LT_JIT_SYNC), 'set_jit_mode')
+
+    def jit_prepare(self, scene, params, bands, valid, fields, index, wait=True):
+        """Compile (wait) or start compiling the JIT module lt_analyze_tiles would use for a tile
+        of these band planes, mask and output fields, carrying `index` (an IndexFn). Raises
+        LtError when a waited-for compile fails (the launches would then fall back)."""
+        P = bands.shape[-1]
+        tin, _, _ = self._tile_structs(scene, params, bands, valid, (), {}, None, index)
+        tout = _abi.LtTileOut()
+        tout.stride = P
+        for f in fields:  # which planes are requested is all the module depends on (never read)
+            setattr(tout, f, ctypes.cast(ctypes.c_void_p(16), type(getattr(tout, f))))
+        sc = scene.to_c()
+        with torch.cuda.device(self.device):
+            self._check(self.lib.lt_jit_prepare(self.ctx, ctypes.byref(sc), ctypes.byref(params),
+                                                ctypes.byref(tin), ctypes.byref(tout),
+                                                1 if wait else 0), 'lt_jit_prepare')
+
+    def jit_stats(self):
+        """The context's JIT counters (lt_jit_stats) and its last JIT failure message."""
+        st = _abi.LtJitStats()
+        msg = ctypes.create_string_buffer(2048)
+        self._check(self.lib.lt_ctx_jit_stats(self.ctx, ctypes.byref(st), msg, len(msg)),
+                    'jit_stats')
+        d = {f: getattr(st, f) for f, _ in _abi.LtJitStats._fields_}
+        d['last_error'] = msg.value.decode(errors='replace')
+        return d
+
     # --- stage timing (HIP events recorded around every launch on the launch stream) ---
     def set_timing(self, enable):
         self._check(self.lib.lt_ctx_set_timing(self.ctx, 1 if enable else 0), 'set_timing')

@@ -196,6 +196,12 @@ class LocalJob:
         # trendlines
         runner = MosaicRunner(eng, m, params, items, label_fields + tl_fields, fn, dist,
                               exchange_fields=label_fields, ring=3 if cuda else 0)
+        # the JIT module compiles on a worker thread while the first tiles run on the precompiled
+        # kernels (same results): a job never stalls ~10 s for hiprtc (LT_JOB_JIT_SYNC=1: waits)
+        jit_async = cuda and runner.jit is not None and os.environ.get('LT_JOB_JIT_SYNC') != '1'
+        if jit_async:
+            eng.set_jit_mode(True)
+            runner.prepare_jit(wait=False)
 
         def sink(f, row, view, t):  # one completed year row of tile t
             host[f][row, t.p0:t.p1] = view.numpy().view(host[f].dtype)
@@ -210,6 +216,9 @@ class LocalJob:
         # tile k-1's rows are queued behind tile k's kernels, so the copies overlap them
         runner.step(after_tile=(lambda k: push(k - 1) if k > 0 else None) if cuda else None,
                     slab_free=copied.get if cuda else None)
+        if jit_async:
+            eng.set_jit_mode(False)
+            self.jit_stats = eng.jit_stats()
         if cuda:
             if items:
                 push(len(items) - 1)

@@ -74,6 +74,7 @@ class MosaicRunner:
                                       engine.device, dist, dst)
         W = mosaic.tile
         self.ring = max(0, int(ring))
+        self._ring_last = {}  # ring slot -> (slab_free of its step, tile) of its last user
 
         def planes():
             return {f: torch.empty((W,) if rows(f) is None else (rows(f), W), dtype=_DTYPE[f],
@@ -115,6 +116,20 @@ class MosaicRunner:
                             if self.cuda and has_bands and load_stream and not self.fused
                             else None)
         self.index_events = []  # (start, stop) pairs of the timed steps' load kernels
+
+    def prepare_jit(self, wait=True):
+        """Compile (wait) or start compiling the JIT module of every scene this rank's tiles
+        belong to before the first step, so no launch waits for hiprtc (a mosaic with several
+        scenes compiles them side by side with wait=False under engine.set_jit_mode(True))."""
+        if self.jit is None:
+            return
+        seen = set()
+        for it in self.items:
+            if it.tile.scene in seen:
+                continue
+            seen.add(it.tile.scene)
+            self.eng.jit_prepare(it.scene, self.params, it.bands, it.valid, self.fields, self.jit,
+                                 wait=wait)
 
     def _groups(self):
         """Consecutive items of one scene, at most self.group per call."""
@@ -226,11 +241,19 @@ class MosaicRunner:
         self.exchange.wait()
 
     def _wait_ring(self, k):
-        """Tile k reuses the ring buffer of tile k - ring: the current stream waits until that
-        tile's planes have been copied out."""
-        if not self.ring or not self.cuda or k < self.ring:
+        """Tile k reuses the ring buffer k % ring: the current stream waits until the planes of
+        the tile that last used it — tile k - ring of this step, or for k < ring one of the
+        previous step's last tiles (a second step() on a ring runner) — have been
+        copied out, as the slab_free of that tile's step reports."""
+        if not self.ring or not self.cuda:
             return
-        ev = self._slab_free(k - self.ring)
+        slot = k % self.ring
+        last = self._ring_last.get(slot)
+        self._ring_last[slot] = (self._slab_free, k)
+        if last is None:
+            return
+        free, j = last
+        ev = free(j)
         if ev is not None:
             torch.cuda.current_stream(self.eng.device).wait_event(ev)
 

@@ -46,7 +46,7 @@ def test_struct_layouts_match_header():
     checks = {
         'lt_rule': _abi.LtRule, 'lt_params': _abi.LtParams, 'lt_scene': _abi.LtScene,
         'lt_tile_in': _abi.LtTileIn, 'lt_tile_out': _abi.LtTileOut,
-        'lt_label_in': _abi.LtLabelIn,
+        'lt_label_in': _abi.LtLabelIn, 'lt_jit_stats': _abi.LtJitStats,
     }
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "%s"' % HEADER,
              'int main(void){']
@@ -155,3 +155,45 @@ def test_parse_date_strict():
     for bad in ['2014/07/01', '14-07-01', 'x', '2014-02-30']:
         with pytest.raises(ValueError):
             parse_date(bad)
+
+
+def _c2_jit_source(flags=_abi.LT_JIT_SRC_SPEC | _abi.LT_JIT_SRC_SCENE):
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, 'tools'))
+    import jit_isa
+    return jit_isa, jit_isa.jit_source('c2', flags=flags)
+
+
+def test_jit_source_is_host_only_and_self_contained():
+    """lt_jit_source (ABI 7) gives, without a GPU, the module source a c2 launch compiles: the
+    launch constants and the scene's tables as literals, the kernel headers included by their bare
+    names (the copies embedded in the library), no path into the source tree."""
+    _, src = _c2_jit_source()
+    assert 'lt_jit_analyze' in src and 'lt_jit_resolve' in src
+    assert '#define LT_SPEC_Y 30' in src and 'lt_spec_scene' in src
+    assert '#include "lt_kernels_dev.h"' in src and '../' not in src
+    _, generic = _c2_jit_source(0)
+    assert 'LT_SPEC_Y' not in generic and 'lt_spec_scene' not in generic
+
+
+def test_library_embeds_the_current_kernel_headers(tmp_path):
+    """liblt_hip.so carries the JIT kernel headers it was built with (the JIT kernels
+    must read the struct layouts of the library's host code): the embedded copies, regenerated
+    from the headers on disk now, are byte for byte inside the library — a header edited without
+    a rebuild fails here."""
+    import __graft_entry__ as ge
+    inc = ge.embed_headers(out=str(tmp_path / 'e.inc'))
+    blob = open(_abi.LIB_PATH, 'rb').read()
+    for rel in ge.JIT_HEADERS:
+        text = open(os.path.join(ROOT, rel)).read().replace(
+            '#include "../../include/lt_abi.h"', '#include "lt_abi.h"')
+        assert text.encode() in blob, rel
+    assert open(inc).read() == open(ge.EMBED_INC).read()
+
+
+def test_jit_module_compiles_on_the_host():
+    """The c2 JIT module compiles with hiprtc for gfx950 on this CPU-only host from the headers as
+    they are embedded (the build check of the code the GPU compiles at run time)."""
+    jit_isa, src = _c2_jit_source()
+    code = jit_isa.hiprtc_compile(src)
+    assert len(code) > 10000 and code[:4] == b'\x7fELF'
