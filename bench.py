@@ -391,11 +391,15 @@ def main():
                           load_stream=not args.serial_load, group=args.group)
     gather = world > 1 and not args.no_gather
 
+    # the JIT module of every scene this rank runs, compiled before the warmup (lt_jit_prepare):
+    # no step waits for hiprtc, and no timed tile may run on the precompiled fallback
+    runner.prepare_jit(wait=True)
     for _ in range(args.warmup):
         runner.step()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
+    jit0 = eng.jit_stats()
     eng.set_timing(True)
     eng.stage_ms()  # reset
     torch.cuda.synchronize()
@@ -408,6 +412,12 @@ def main():
         dist.barrier()
     stages = eng.stage_ms()
     eng.set_timing(False)
+    jit1 = eng.jit_stats()
+    jit = {'tiles_jit_timed': jit1['jit_tiles'] - jit0['jit_tiles'],
+           'tiles_fallback_timed': jit1['fallback_tiles'] - jit0['fallback_tiles'],
+           'modules': jit1['modules'], 'compiles': jit1['compiles'],
+           'disk_hits': jit1['disk_hits'], 'failures': jit1['failures'],
+           'override': os.environ.get('LT_JIT_OVERRIDE_DIR')}
     n_deferred_last = eng.last_deferred()
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
     if dist is not None:
@@ -595,6 +605,7 @@ def main():
                      # launch time: a work-equivalent speed, not a fraction of any peak (the
                      # kernel proves most candidate fits irrelevant and never computes them)
                      'reference_work_equivalent_tflops': round(ref_equiv, 2)},
+        'jit': jit,
         'status_numeric_pixels': n_numeric,
         'parity_sample': psample,
         'exchange_check': xcheck,

@@ -1005,9 +1005,13 @@ int lt_jit_source(const lt_scene* sc, const lt_params* prm, const lt_index_prog*
     if (flags & LT_JIT_SRC_SCENE) sp.scene = &tmp;
   }
   std::string err;
-  const std::string src =
-      lt_jit::source(*prog, maxy, rmax, lt_jit::series_type(prog->out_type, n_rules), sp, err);
+  const char* vt = lt_jit::series_type(prog->out_type, n_rules);
+  const std::string src = lt_jit::source(*prog, maxy, rmax, vt, sp, err);
   if (src.empty()) return LT_ERR_ARG;
+  // the context's module key of this specialisation (hashed here too, so the host-only tests
+  // exercise it)
+  volatile uint64_t key = lt_jit::spec_key(*prog, maxy, rmax, vt, sp);
+  (void)key;
   if (buf && cap > 0) {
     const size_t n = src.size() < (size_t)(cap - 1) ? src.size() : (size_t)(cap - 1);
     memcpy(buf, src.data(), n);

@@ -90,7 +90,7 @@ inline bool read_file(const std::string& path, std::string& out) {
   return true;
 }
 
-inline uint64_t fnv1a(const void* p, size_t n, uint64_t h = 1469598103934665603ull) {
+inline uint64_t fnv1a_bytes(const void* p, size_t n, uint64_t h = 1469598103934665603ull) {
   const unsigned char* c = (const unsigned char*)p;
   for (size_t i = 0; i < n; i++) {
     h ^= c[i];
@@ -99,7 +99,7 @@ inline uint64_t fnv1a(const void* p, size_t n, uint64_t h = 1469598103934665603u
   return h;
 }
 inline uint64_t fnv1a(const std::string& s, uint64_t h = 1469598103934665603ull) {
-  return fnv1a(s.data(), s.size(), h);
+  return fnv1a_bytes(s.data(), s.size(), h);
 }
 
 struct Headers {
@@ -150,7 +150,7 @@ inline bool headers(Headers& H, std::string& err) {
         H.text[i].replace(at, rel.size(), "#include \"lt_abi.h\"");
     }
   }
-  uint64_t h = fnv1a(H.embedded ? "embedded" : "disk");
+  uint64_t h = fnv1a(std::string(H.embedded ? "embedded" : "disk"));
   for (const std::string& t : H.text) h = fnv1a(t, h);
   H.hash = h;
   return true;
@@ -240,7 +240,7 @@ inline std::string fmt_rule(const lt_rule& r) {
 // compile-time switches, LT_JIT_WAVES the analyze kernel's occupancy): part of spec_key
 inline std::string env_switches() {
   std::string r;
-  for (const char* v : {"LT_JIT_DEFINES", "LT_JIT_WAVES"}) {
+  for (const char* v : {"LT_JIT_DEFINES", "LT_JIT_WAVES", "LT_JIT_OVERRIDE_DIR"}) {
     const char* e = getenv(v);
     r += std::string(v) + "=" + (e ? e : "") + ";";
   }
@@ -252,46 +252,46 @@ inline std::string env_switches() {
 // formatting and comparing the whole source)
 inline uint64_t spec_key(const lt_index_prog& P, int maxy, int rmax, const char* vt,
                          const Spec& sp) {
-  uint64_t h = fnv1a(&P.n_ops, sizeof P.n_ops);
-  h = fnv1a(&P.n_bands, sizeof P.n_bands, h);
-  h = fnv1a(&P.band_type, sizeof P.band_type, h);
-  h = fnv1a(&P.out_type, sizeof P.out_type, h);
+  uint64_t h = fnv1a_bytes(&P.n_ops, sizeof P.n_ops);
+  h = fnv1a_bytes(&P.n_bands, sizeof P.n_bands, h);
+  h = fnv1a_bytes(&P.band_type, sizeof P.band_type, h);
+  h = fnv1a_bytes(&P.out_type, sizeof P.out_type, h);
   for (int i = 0; i < P.n_ops && i < LT_MAX_PROG; i++) {
     const lt_index_op& o = P.ops[i];
-    h = fnv1a(&o.op, sizeof o.op, h);
-    h = fnv1a(&o.type, sizeof o.type, h);
-    h = fnv1a(&o.ival, sizeof o.ival, h);
-    h = fnv1a(&o.fval, sizeof o.fval, h);
+    h = fnv1a_bytes(&o.op, sizeof o.op, h);
+    h = fnv1a_bytes(&o.type, sizeof o.type, h);
+    h = fnv1a_bytes(&o.ival, sizeof o.ival, h);
+    h = fnv1a_bytes(&o.fval, sizeof o.fval, h);
   }
   const int inst[3] = {maxy, rmax, (int)strlen(vt)};
-  h = fnv1a(inst, sizeof inst, fnv1a(vt, h));
+  h = fnv1a_bytes(inst, sizeof inst, fnv1a(std::string(vt), h));
   const int flags[4] = {sp.on ? 1 : 0, sp.n_years, sp.masked ? 1 : 0, sp.year_out ? 1 : 0};
-  h = fnv1a(flags, sizeof flags, h);
+  h = fnv1a_bytes(flags, sizeof flags, h);
   if (sp.on) {
     const lt_params& Q = sp.params;
-    h = fnv1a(&Q.line_cost, sizeof Q.line_cost, h);
-    h = fnv1a(&Q.n_rules, sizeof Q.n_rules, h);
-    h = fnv1a(&Q.pre_threshold_mode, sizeof Q.pre_threshold_mode, h);
+    h = fnv1a_bytes(&Q.line_cost, sizeof Q.line_cost, h);
+    h = fnv1a_bytes(&Q.n_rules, sizeof Q.n_rules, h);
+    h = fnv1a_bytes(&Q.pre_threshold_mode, sizeof Q.pre_threshold_mode, h);
     for (int r = 0; r < Q.n_rules && r < LT_MAX_RULES; r++) {
       const lt_rule& u = Q.rules[r];
       const int32_t ints[5] = {u.change_type, u.onset_op, u.duration_op, u.pre_op, u.class_val};
       const double dbl[3] = {u.onset_val, u.duration_val, u.pre_val};
-      h = fnv1a(dbl, sizeof dbl, fnv1a(ints, sizeof ints, h));
+      h = fnv1a_bytes(dbl, sizeof dbl, fnv1a_bytes(ints, sizeof ints, h));
     }
   }
   if (sp.on && sp.scene) {
     const lt::DevScene& S = *sp.scene;
-    h = fnv1a(&S.n_obs, sizeof S.n_obs, h);
-    h = fnv1a(&S.n_years, sizeof S.n_years, h);
-    h = fnv1a(&S.feb29_mask, sizeof S.feb29_mask, h);
+    h = fnv1a_bytes(&S.n_obs, sizeof S.n_obs, h);
+    h = fnv1a_bytes(&S.n_years, sizeof S.n_years, h);
+    h = fnv1a_bytes(&S.feb29_mask, sizeof S.feb29_mask, h);
     const int Y = S.n_years, K = S.n_obs;
-    h = fnv1a(S.year, sizeof(int32_t) * Y, h);
-    h = fnv1a(S.slot_begin, sizeof(int32_t) * (Y + 1), h);
-    h = fnv1a(S.order, sizeof(int32_t) * K, h);
-    h = fnv1a(S.dist, sizeof(int32_t) * K, h);
-    h = fnv1a(S.winner_all, sizeof(int32_t) * Y, h);
+    h = fnv1a_bytes(S.year, sizeof(int32_t) * Y, h);
+    h = fnv1a_bytes(S.slot_begin, sizeof(int32_t) * (Y + 1), h);
+    h = fnv1a_bytes(S.order, sizeof(int32_t) * K, h);
+    h = fnv1a_bytes(S.dist, sizeof(int32_t) * K, h);
+    h = fnv1a_bytes(S.winner_all, sizeof(int32_t) * Y, h);
   } else {
-    h = fnv1a("no-scene", h);
+    h = fnv1a(std::string("no-scene"), h);
   }
   return fnv1a(env_switches(), h);
 }
@@ -385,7 +385,7 @@ inline uint64_t env_key(const Headers& H, const std::vector<std::string>& opts) 
   (void)hiprtcVersion(&maj, &min);
   (void)hipRuntimeGetVersion(&rt);
   const int v[3] = {maj, min, rt};
-  return fnv1a(v, sizeof v, h);
+  return fnv1a_bytes(v, sizeof v, h);
 }
 
 inline std::vector<std::string> options(const std::string& arch) {
@@ -398,6 +398,16 @@ inline std::vector<std::string> options(const std::string& arch) {
 inline bool compile(const std::string& src, const std::string& arch, std::string& code,
                     bool& disk_hit, std::string& err) {
   disk_hit = false;
+  // A/B runs of post-compile variants (tools/jit_asm.py): LT_JIT_OVERRIDE_DIR/lt_src_<FNV-1a of
+  // the source>.co is loaded instead of compiling this source
+  if (const char* od = getenv("LT_JIT_OVERRIDE_DIR")) {
+    char nm[64];
+    snprintf(nm, sizeof nm, "/lt_src_%016llx.co", (unsigned long long)fnv1a(src));
+    if (read_file(std::string(od) + nm, code) && !code.empty()) {
+      disk_hit = true;
+      return true;
+    }
+  }
   Headers H;
   if (!headers(H, err)) return false;
   const std::vector<std::string> opts = options(arch);

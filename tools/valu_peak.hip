@@ -44,20 +44,28 @@
 //   mov_b64               v_mov_b64 (gfx950's 64-bit move)
 //   cmp_e32               VOPC e32 compares writing VCC (back to back)
 //   nop_mix               one s_nop 0 per eight v_add_u32 (the hazard padding the compiler emits)
+// Round-5 second set (e32 selects on a VCC not written by the instruction before them measured 16
+// cycles, VALU-written, and 23, SALU-written; the compiler's compare -> select pair 4.1):
+//   cmp_cnd2_vcc          v_cmp_e32 (VCC) then TWO e32 selects on it (a binary64 select), 8 chains
+//   cmp_cnd4_vcc          v_cmp_e32 (VCC) then FOUR e32 selects on it
+//   cmp_gap_cnd_vcc       v_cmp_e32 (VCC), three independent v_add_u32, then one e32 select
+//   cmp64_cnd2            v_cmp_e64 into an SGPR pair, then two e64 selects on it
 enum Kind { ADD_U32, CNDMASK, CMP, FMA_F32, FMA_F32K, ADD_F64, FMA_F64, MUL_F64, RCP_F64, LSHL_B64,
             MIX_C2, MOV_B32, CNDMASK_VCC, CNDMASK_VCC_VALU, CMP_CNDMASK_VCC, CNDMASK_E64_VCC,
-            CNDMASK_E64_SMOV, CNDMASK_E64_VCMP, MOV_B64, CMP_E32, NOP_MIX, NKIND };
+            CNDMASK_E64_SMOV, CNDMASK_E64_VCMP, MOV_B64, CMP_E32, NOP_MIX, CMP_CND2_VCC,
+            CMP_CND4_VCC, CMP_GAP_CND_VCC, CMP64_CND2, NKIND };
 static const char* kKindName[NKIND] = {"add_u32", "cndmask_b32", "cmp_gt_u32", "fma_f32",
                                        "fma_f32_k", "add_f64", "fma_f64", "mul_f64", "rcp_f64",
                                        "lshlrev_b64", "mix_c2", "mov_b32", "cndmask_b32_vcc",
                                        "cndmask_vcc_valu", "cmp_cndmask_vcc", "cndmask_e64_vcc",
                                        "cndmask_e64_smov", "cndmask_e64_vcmp", "mov_b64",
-                                       "cmp_e32", "nop_mix"};
+                                       "cmp_e32", "nop_mix", "cmp_cnd2_vcc", "cmp_cnd4_vcc",
+                                       "cmp_gap_cnd_vcc", "cmp64_cnd2"};
 // VALU / SALU instructions per loop iteration of each kind (the asm blocks below)
 static const int kValuPerIter[NKIND] = {64, 64, 64, 64, 64, 64, 64, 64, 32, 64, 103, 64, 64,
-                                        65, 64, 64, 64, 65, 64, 64, 64};
+                                        65, 64, 64, 64, 65, 64, 64, 64, 48, 80, 80, 48};
 static const int kSaluPerIter[NKIND] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 50, 0, 1,
-                                        0, 0, 1, 1, 0, 0, 0, 8};
+                                        0, 0, 1, 1, 0, 0, 0, 8, 0, 0, 0, 0};
 
 #define R8(s) s s s s s s s s
 
@@ -186,6 +194,60 @@ __global__ void __launch_bounds__(64) valu_kernel(unsigned* out, unsigned long l
                       "s_nop 0\n")
                    : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)
                    : "v"(inc));
+    } else if constexpr (K == CMP_CND2_VCC) {  // compare, then a pair of selects on its VCC
+#define P2(a, b) "v_cmp_gt_u32_e32 vcc, %8, " a "\n v_cndmask_b32_e32 " a ", " a ", %8, vcc\n" \
+                 " v_cndmask_b32_e32 " b ", " b ", %8, vcc\n"
+      asm volatile(P2("%0", "%1") P2("%2", "%3") P2("%4", "%5") P2("%6", "%7")
+                   P2("%1", "%0") P2("%3", "%2") P2("%5", "%4") P2("%7", "%6")
+                   P2("%0", "%1") P2("%2", "%3") P2("%4", "%5") P2("%6", "%7")
+                   P2("%1", "%0") P2("%3", "%2") P2("%5", "%4") P2("%7", "%6")
+                   : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)
+                   : "v"(inc)
+                   : "vcc");
+#undef P2
+    } else if constexpr (K == CMP_CND4_VCC) {  // compare, then four selects on its VCC
+#define P4(a, b, c, d) "v_cmp_gt_u32_e32 vcc, %8, " a "\n v_cndmask_b32_e32 " a ", " a ", %8, vcc\n" \
+                       " v_cndmask_b32_e32 " b ", " b ", %8, vcc\n v_cndmask_b32_e32 " c ", " c \
+                       ", %8, vcc\n v_cndmask_b32_e32 " d ", " d ", %8, vcc\n"
+      asm volatile(P4("%0", "%1", "%2", "%3") P4("%4", "%5", "%6", "%7")
+                   P4("%1", "%2", "%3", "%0") P4("%5", "%6", "%7", "%4")
+                   P4("%2", "%3", "%0", "%1") P4("%6", "%7", "%4", "%5")
+                   P4("%3", "%0", "%1", "%2") P4("%7", "%4", "%5", "%6")
+                   P4("%0", "%1", "%2", "%3") P4("%4", "%5", "%6", "%7")
+                   P4("%1", "%2", "%3", "%0") P4("%5", "%6", "%7", "%4")
+                   P4("%2", "%3", "%0", "%1") P4("%6", "%7", "%4", "%5")
+                   P4("%3", "%0", "%1", "%2") P4("%7", "%4", "%5", "%6")
+                   : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)
+                   : "v"(inc)
+                   : "vcc");
+#undef P4
+    } else if constexpr (K == CMP_GAP_CND_VCC) {  // compare, three independent adds, one select
+#define G1(a, x, y, z) "v_cmp_gt_u32_e32 vcc, %8, " a "\n v_add_u32 " x ", " x ", %8\n" \
+                       " v_add_u32 " y ", " y ", %8\n v_add_u32 " z ", " z ", %8\n" \
+                       " v_cndmask_b32_e32 " a ", " a ", %8, vcc\n"
+      asm volatile(G1("%0", "%1", "%2", "%3") G1("%4", "%5", "%6", "%7")
+                   G1("%1", "%2", "%3", "%0") G1("%5", "%6", "%7", "%4")
+                   G1("%2", "%3", "%0", "%1") G1("%6", "%7", "%4", "%5")
+                   G1("%3", "%0", "%1", "%2") G1("%7", "%4", "%5", "%6")
+                   G1("%0", "%1", "%2", "%3") G1("%4", "%5", "%6", "%7")
+                   G1("%1", "%2", "%3", "%0") G1("%5", "%6", "%7", "%4")
+                   G1("%2", "%3", "%0", "%1") G1("%6", "%7", "%4", "%5")
+                   G1("%3", "%0", "%1", "%2") G1("%7", "%4", "%5", "%6")
+                   : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)
+                   : "v"(inc)
+                   : "vcc");
+#undef G1
+    } else if constexpr (K == CMP64_CND2) {  // e64 compare into an SGPR pair, two e64 selects
+#define Q2(a, b) "v_cmp_gt_u32_e64 %8, %9, " a "\n v_cndmask_b32_e64 " a ", " a ", %9, %8\n" \
+                 " v_cndmask_b32_e64 " b ", " b ", %9, %8\n"
+      asm volatile(Q2("%0", "%1") Q2("%2", "%3") Q2("%4", "%5") Q2("%6", "%7")
+                   Q2("%1", "%0") Q2("%3", "%2") Q2("%5", "%4") Q2("%7", "%6")
+                   Q2("%0", "%1") Q2("%2", "%3") Q2("%4", "%5") Q2("%6", "%7")
+                   Q2("%1", "%0") Q2("%3", "%2") Q2("%5", "%4") Q2("%7", "%6")
+                   : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7),
+                     "=&s"(m0)
+                   : "v"(inc));
+#undef Q2
     } else if constexpr (K == FMA_F32K) {  // two VGPR sources and an inline constant
       asm volatile(R8("v_fma_f32 %0, %0, %8, 0.5\n v_fma_f32 %1, %1, %8, 0.5\n v_fma_f32 %2, %2, %8, 0.5\n"
                       "v_fma_f32 %3, %3, %8, 0.5\n v_fma_f32 %4, %4, %8, 0.5\n v_fma_f32 %5, %5, %8, 0.5\n"
@@ -292,6 +354,10 @@ static KFn kernel_of(int k) {
     case MOV_B64: return valu_kernel<MOV_B64>;
     case CMP_E32: return valu_kernel<CMP_E32>;
     case NOP_MIX: return valu_kernel<NOP_MIX>;
+    case CMP_CND2_VCC: return valu_kernel<CMP_CND2_VCC>;
+    case CMP_CND4_VCC: return valu_kernel<CMP_CND4_VCC>;
+    case CMP_GAP_CND_VCC: return valu_kernel<CMP_GAP_CND_VCC>;
+    case CMP64_CND2: return valu_kernel<CMP64_CND2>;
     default: return valu_kernel<MIX_C2>;
   }
 }
