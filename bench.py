@@ -626,6 +626,10 @@ def main():
                       'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                       'frac': round(index_bytes / (index_alone_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                                     4)}},
+        'expand_stage': {'ms_per_launch': round(stages.get('expand', 0.0) / n_launch, 3),
+                         'kernel': 'trendline_expand_kernel (per-year planes from the compact '
+                                   'trendline, on its own stream beside the next analyze)'}
+        if cfg['trendline'] else None,
         'resolve_stage': {'ms_per_launch': round(resolve_ms, 3),
                           'deferred_pixels_last_tile': n_deferred_last,
                           'last_tile_pixels': items[-1].tile.n},

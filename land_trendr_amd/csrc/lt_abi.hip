@@ -90,6 +90,73 @@ __global__ __launch_bounds__(kBlock) void year_flags_kernel(const uint64_t* __re
   }
 }
 
+// The per-year trendline planes from the compact trendline the analyze / resolve stages leave
+// (lt_fast.h tl_split): eqns2fitted_points (utils.py:682-722) and the TrendlinePoint fields
+// (classes.py:67-116) of year slot y = blockIdx.y for one pixel per thread. Everything follows
+// from the pixel's four words — present years P0 (0: the reference raises), spike flags by present
+// index, vertices by non-spike index, the left-eqn choice by vertex number — and at most two
+// segment eqns:
+//   t = present index of slot y, spike = bit t, k = its non-spike index, vertex = bit k;
+//   passed = vertices at or before the point; the current eqn is segment passed-1, or, past the
+//   last vertex (whose eqn is its left segment's, utils.py:662), segment n_vertices-2;
+//   val_fit = m x + b of the current eqn (x = year offset from the first present year, no FMA),
+//   or of the previous one at an interior vertex that took the left eqn;
+//   fit_m / fit_b = the eqn used, right_m / right_b = the current one; NaN for absent years.
+// Exactly the values of the year-major loop (lt_fast.h, tl_split off), which it replaces. Each
+// thread only loads, then stores: no store-then-load order inside a thread. Rows: 256 pixels of
+// one year per block, so every plane row is written in 2 KB (binary64) / 256 B (u8) runs.
+__global__ __launch_bounds__(kBlock) void trendline_expand_kernel(
+    const lt::DevScene* __restrict__ S, const uint64_t* __restrict__ bits,
+    const double* __restrict__ eqn, int64_t n, const lt_tile_out out) {
+  const int y = blockIdx.y;
+  const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (p >= n) return;
+  const uint64_t P0 = __builtin_nontemporal_load(bits + p);
+  const double nan = __builtin_nan("");
+  double fv = nan, fm = nan, fb = nan, rm = nan, rb = nan;
+  uint8_t sp = 0, vx = 0;
+  if ((P0 >> y) & 1) {
+    const uint64_t SP = __builtin_nontemporal_load(bits + n + p);
+    const uint64_t VM = __builtin_nontemporal_load(bits + 2 * n + p);
+    const uint64_t LB = __builtin_nontemporal_load(bits + 3 * n + p);
+    const int t = __builtin_popcountll(P0 & ((1ull << y) - 1));  // y <= 63
+    sp = (uint8_t)((SP >> t) & 1);
+    const int k = t - __builtin_popcountll(SP & ((1ull << t) - 1));
+    vx = (uint8_t)(!sp && ((VM >> k) & 1));
+    const int nvt = __builtin_popcountll(VM);
+    const uint64_t upto = sp ? ((1ull << k) - 1) : (k >= 63 ? ~0ull : ((2ull << k) - 1));
+    const int qc = __builtin_popcountll(VM & upto) - 1;  // the last vertex at or before the point
+    const int e = qc + 1 >= nvt ? nvt - 2 : qc;
+    double cm = 0.0, cb = 0.0;
+    typedef double d2 __attribute__((ext_vector_type(2)));
+    if (e >= 0) {
+      const d2 v = *(const d2*)(eqn + 2 * ((int64_t)e * n + p));
+      cm = v.x;
+      cb = v.y;
+    }
+    const double x = (double)(S->year[y] - S->year[__builtin_ctzll(P0)]);
+    fv = (cm * x) + cb;
+    fm = cm;
+    fb = cb;
+    rm = cm;
+    rb = cb;
+    if (vx && qc > 0 && qc < nvt - 1 && ((LB >> qc) & 1)) {
+      const d2 v = *(const d2*)(eqn + 2 * ((int64_t)(qc - 1) * n + p));
+      fv = (v.x * x) + v.y;
+      fm = v.x;
+      fb = v.y;
+    }
+  }
+  const int64_t o = (int64_t)y * out.stride + p;
+  if (out.val_fit) __builtin_nontemporal_store(fv, out.val_fit + o);
+  if (out.fit_m) __builtin_nontemporal_store(fm, out.fit_m + o);
+  if (out.fit_b) __builtin_nontemporal_store(fb, out.fit_b + o);
+  if (out.right_m) __builtin_nontemporal_store(rm, out.right_m + o);
+  if (out.right_b) __builtin_nontemporal_store(rb, out.right_b + o);
+  if (out.spike) out.spike[o] = sp;
+  if (out.vertex) out.vertex[o] = vx;
+}
+
 struct YearArg {
   int32_t year[LT_MAX_YEARS];
 };
@@ -206,6 +273,17 @@ struct lt_ctx {
   // the precompiled fallback of a non-linear program: its index raster per deferred-list set
   void* d_iscratch[kSets] = {};
   size_t iscratch_bytes[kSets] = {};
+  // the compact trendline per deferred-list set (lt_fast.h tl_split): [4][cap] words and
+  // [Y-1][cap] segment eqns, written by analyze / resolve, read by trendline_expand_kernel
+  uint64_t* d_tl_bits[kSets] = {};
+  double* d_tl_eqn[kSets] = {};
+  int64_t tl_cap[kSets] = {};
+  int tl_segs[kSets] = {};
+  hipStream_t xstream = nullptr;  // the expand kernel's stream (LT_EXPAND_PRIORITY)
+  hipEvent_t ev_rdone[kSets] = {};  // a tile's resolve kernels done (the expand kernel waits)
+  hipEvent_t ev_xdone = nullptr;    // the last expand kernel queued
+  bool x_used = false;
+  bool tl_split = true;  // LT_TL_SPLIT at creation
 };
 
 static int fail(lt_ctx* c, int code, const char* fmt, const char* detail = "") {
@@ -260,6 +338,7 @@ int lt_ctx_create(int device, lt_ctx** out) {
     if (atoi(e) >= 1) c->jit_max_modules = atoi(e);
   if (const char* e = getenv("LT_JIT_SCENE_MAX"))
     if (atoi(e) >= 0) c->jit_scene_max = atoi(e);
+  if (const char* e = getenv("LT_TL_SPLIT")) c->tl_split = e[0] != '0';
   hipError_t e = hipSetDevice(device);
   if (e == hipSuccess) e = hipHostMalloc((void**)&c->h_scene, sizeof(lt::DevScene));
   if (e == hipSuccess) e = hipMalloc((void**)&c->d_scene, sizeof(lt::DevScene));
@@ -303,8 +382,17 @@ int lt_ctx_destroy(lt_ctx* c) {
     if (kv.second.ev_last) (void)hipEventDestroy(kv.second.ev_last);
     if (kv.second.k.mod) (void)hipModuleUnload(kv.second.k.mod);
   }
-  for (int s = 0; s < lt_ctx::kSets; s++)
+  if (c->xstream) {
+    (void)hipStreamSynchronize(c->xstream);
+    (void)hipStreamDestroy(c->xstream);
+  }
+  if (c->ev_xdone) (void)hipEventDestroy(c->ev_xdone);
+  for (int s = 0; s < lt_ctx::kSets; s++) {
     if (c->d_iscratch[s]) (void)hipFree(c->d_iscratch[s]);
+    if (c->d_tl_bits[s]) (void)hipFree(c->d_tl_bits[s]);
+    if (c->d_tl_eqn[s]) (void)hipFree(c->d_tl_eqn[s]);
+    if (c->ev_rdone[s]) (void)hipEventDestroy(c->ev_rdone[s]);
+  }
   if (c->d_defer) (void)hipFree(c->d_defer);
   if (c->d_yflags) (void)hipFree(c->d_yflags);
   if (c->d_ndefer) (void)hipFree(c->d_ndefer);
@@ -330,14 +418,14 @@ int lt_ctx_set_timing(lt_ctx* c, int enable) {
 int lt_ctx_stage_ms(lt_ctx* c, double* ms_out, int n_stages, int64_t* n_launches) {
   if (!c) return LT_ERR_ARG;
   HIP_OR_FAIL(c, hipSetDevice(c->device));
-  double acc[2] = {0.0, 0.0};
+  double acc[3] = {0.0, 0.0, 0.0};
   for (size_t i = 0; i < c->used; i++) {
     HIP_OR_FAIL(c, hipEventSynchronize(c->pool[i].stop));
     float ms = 0.f;
     HIP_OR_FAIL(c, hipEventElapsedTime(&ms, c->pool[i].start, c->pool[i].stop));
-    acc[i & 1] += ms;  // pairs alternate: analyze stage, resolve stage
+    acc[i % 3] += ms;  // pairs cycle: analyze stage, resolve stage, trendline expand
   }
-  for (int s = 0; s < n_stages; s++) ms_out[s] = s < 2 ? acc[s] : 0.0;
+  for (int s = 0; s < n_stages; s++) ms_out[s] = s < 3 ? acc[s] : 0.0;
   if (n_launches) *n_launches = c->launches;
   c->used = 0;
   c->launches = 0;
@@ -381,6 +469,14 @@ static int check_tile(lt_ctx* c, const lt_tile_in* in, const lt_tile_out* out) {
   if (in->obs_index && !lt_idx::ctype(in->index_type))
     return fail(c, LT_ERR_ARG, "bad index_type%s");
   return LT_OK;
+}
+
+// Per-year planes with the compact trendline (lt_fast.h tl_split, trendline_expand_kernel):
+// every launch asking for any of them, unless the context was created with LT_TL_SPLIT=0 (A/B
+// runs and tests: the year-major loop)
+static bool tl_split_launch(const lt_ctx* c, const lt_tile_out* o) {
+  return c->tl_split && (o->val_fit || o->fit_m || o->fit_b || o->right_m || o->right_b ||
+                         o->spike || o->vertex);
 }
 
 // the device's target id, for hiprtc (cached)
@@ -466,6 +562,7 @@ static int jit_acquire(lt_ctx* c, const lt_index* f, int Y, const lt_params* prm
     sp.masked = in->obs_valid != nullptr || in->obs_valid_bits != nullptr;
     sp.year_out = o->val_fit || o->fit_m || o->fit_b || o->right_m || o->right_b || o->spike ||
                   o->vertex;
+    sp.tl_split = tl_split_launch(c, o);
     sp.params = *prm;
     if (scene_on) sp.scene = scene;
   }
@@ -580,22 +677,61 @@ static int jit_fallback_tile(lt_ctx* c, const lt_tile_in* in, int n_obs, int set
   return LT_OK;
 }
 
+// set `set`'s compact trendline buffers for defer_cap pixels and Y year slots (Y-1 segments),
+// and the expand stream; a buffer still read by an earlier tile's expand kernel is freed only
+// after it (the set's last user is ordered before this tile by ev_resolved, but a resize frees)
+static int tl_buffers(lt_ctx* c, int set, int Y) {
+  if (!c->xstream) {
+    int least = 0, greatest = 0;
+    HIP_OR_FAIL(c, hipDeviceGetStreamPriorityRange(&least, &greatest));
+    const char* pr = getenv("LT_EXPAND_PRIORITY");  // high / normal / low (A/B runs)
+    const int prio = pr && strcmp(pr, "high") == 0 ? greatest
+                     : pr && strcmp(pr, "low") == 0 ? least : 0;
+    HIP_OR_FAIL(c, hipStreamCreateWithPriority(&c->xstream, hipStreamNonBlocking, prio));
+    HIP_OR_FAIL(c, hipEventCreateWithFlags(&c->ev_xdone, hipEventDisableTiming));
+    for (int s = 0; s < lt_ctx::kSets; s++)
+      HIP_OR_FAIL(c, hipEventCreateWithFlags(&c->ev_rdone[s], hipEventDisableTiming));
+  }
+  const int segs = Y > 1 ? Y - 1 : 1;
+  if (c->tl_cap[set] >= c->defer_cap && c->tl_segs[set] >= segs) return LT_OK;
+  HIP_OR_FAIL(c, hipStreamSynchronize(c->xstream));
+  if (c->d_tl_bits[set]) HIP_OR_FAIL(c, hipFree(c->d_tl_bits[set]));
+  if (c->d_tl_eqn[set]) HIP_OR_FAIL(c, hipFree(c->d_tl_eqn[set]));
+  c->d_tl_bits[set] = nullptr;
+  c->d_tl_eqn[set] = nullptr;
+  c->tl_cap[set] = 0;
+  HIP_OR_FAIL(c, hipMalloc((void**)&c->d_tl_bits[set], 4 * sizeof(uint64_t) * (size_t)c->defer_cap));
+  HIP_OR_FAIL(c, hipMalloc((void**)&c->d_tl_eqn[set],
+                           2 * sizeof(double) * (size_t)segs * (size_t)c->defer_cap));
+  c->tl_cap[set] = c->defer_cap;
+  c->tl_segs[set] = segs;
+  return LT_OK;
+}
+
 // One tile's stages: the analyze kernel on `stream`, the resolve kernels (its deferred pixels) on
 // `rstream` once the analyze kernel is done; deferred-pixel list / counters set `set`.
 static int launch_tile(lt_ctx* c, const lt_params* prm, const lt_tile_in* in,
                        const lt_tile_out* out, int Y, hipStream_t stream, hipStream_t rstream,
                        int set) {
   int64_t* dl = c->d_defer + (size_t)set * 2 * c->defer_cap;
-  // the spike / vertex planes go through per-pixel year flags ([2][n_pix] of this set)
-  uint64_t* yf = (out->spike || out->vertex) ? c->d_yflags + (size_t)set * 2 * c->defer_cap
-                                             : nullptr;
+  // per-year planes requested: with the compact trendline (default) the analyze / resolve
+  // stages leave per-pixel words and segment eqns and trendline_expand_kernel writes every plane
+  // (spike / vertex included); else the year-major loop writes the planes and the spike / vertex
+  // planes go through per-pixel year flags ([2][n_pix] of this set)
+  const bool tl = tl_split_launch(c, out);
+  uint64_t* yf = (!tl && (out->spike || out->vertex))
+                     ? c->d_yflags + (size_t)set * 2 * c->defer_cap : nullptr;
+  if (tl) {
+    const int rc = tl_buffers(c, set, Y);
+    if (rc != LT_OK) return rc;
+  }
   unsigned long long* dn = c->d_ndefer + 4 * set;
   // [0]/[2]: deferred-pixel counts of the binary32 / binary64 lists (stage 1), [1]/[3]: the
   // resolve launches' work counters
   HIP_OR_FAIL(c, hipMemsetAsync(dn, 0, 4 * sizeof(unsigned long long), stream));
-  EventPair* ep[2] = {nullptr, nullptr};
+  EventPair* ep[3] = {nullptr, nullptr, nullptr};
   if (c->timing) {
-    while (c->pool.size() < c->used + 2) {  // grow first: pointers into the pool stay valid
+    while (c->pool.size() < c->used + 3) {  // grow first: pointers into the pool stay valid
       EventPair np;
       HIP_OR_FAIL(c, hipEventCreate(&np.start));
       HIP_OR_FAIL(c, hipEventCreate(&np.stop));
@@ -603,11 +739,16 @@ static int launch_tile(lt_ctx* c, const lt_params* prm, const lt_tile_in* in,
     }
     ep[0] = &c->pool[c->used++];
     ep[1] = &c->pool[c->used++];
+    ep[2] = &c->pool[c->used++];
   }
   if (ep[0]) HIP_OR_FAIL(c, hipEventRecord(ep[0]->start, stream));
   const int64_t nwave = (in->n_pix + 63) / 64;
   if (nwave > 0x7fffffff) return fail(c, LT_ERR_LIMIT, "tile too large%s");
   lt::TileLaunch l{c->d_scene, prm, in, out, c->d_xtab, dl, dn, yf, Y, c->device, stream};
+  if (tl) {
+    l.tl_bits = c->d_tl_bits[set];
+    l.tl_eqn = c->d_tl_eqn[set];
+  }
   const lt_jit_kernels* jk = nullptr;
   JitEntry* je = nullptr;
   lt_tile_in alt;  // the tile as the precompiled kernels read it (JIT kernels not ready)
@@ -628,7 +769,8 @@ static int launch_tile(lt_ctx* c, const lt_params* prm, const lt_tile_in* in,
   // the JIT kernels' one argument, as the product kernels get it (lt_kernels.h kernel_args)
   auto jit_launch = [&](hipFunction_t f, unsigned grid, int64_t* list,
                         unsigned long long* counters, hipStream_t s) -> hipError_t {
-    lt::KernelArgs a{c->d_scene, *prm, *in, *out, c->d_xtab, list, counters, yf};
+    lt::KernelArgs a{c->d_scene, *prm, *in, *out, c->d_xtab, list, counters, yf, l.tl_bits,
+                     l.tl_eqn};
     size_t sz = sizeof a;
     void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz,
                    HIP_LAUNCH_PARAM_END};
@@ -666,6 +808,31 @@ static int launch_tile(lt_ctx* c, const lt_params* prm, const lt_tile_in* in,
     HIP_OR_FAIL(c, lt::launch_resolve(l));
   }
   if (sync_each) HIP_OR_FAIL(c, hipStreamSynchronize(stream));
+  if (tl) {  // every pixel's compact trendline is in (analyze + resolve): the year rows
+    if (ep[1]) HIP_OR_FAIL(c, hipEventRecord(ep[1]->stop, rstream));
+    HIP_OR_FAIL(c, hipEventRecord(c->ev_rdone[set], rstream));
+    HIP_OR_FAIL(c, hipStreamWaitEvent(c->xstream, c->ev_rdone[set], 0));
+    if (ep[2]) HIP_OR_FAIL(c, hipEventRecord(ep[2]->start, c->xstream));
+    if (Y > 0) {
+      dim3 eg((unsigned)((in->n_pix + kBlock - 1) / kBlock), (unsigned)Y), eb(kBlock);
+      hipLaunchKernelGGL(trendline_expand_kernel, eg, eb, 0, c->xstream, c->d_scene, l.tl_bits,
+                         l.tl_eqn, in->n_pix, *out);
+    }
+    HIP_OR_FAIL(c, hipGetLastError());
+    if (ep[2]) HIP_OR_FAIL(c, hipEventRecord(ep[2]->stop, c->xstream));
+    // the set (and the expand kernel's reads of it) is free again after this point
+    HIP_OR_FAIL(c, hipEventRecord(c->ev_resolved[set], c->xstream));
+    HIP_OR_FAIL(c, hipEventRecord(c->ev_xdone, c->xstream));
+    c->x_used = true;
+    if (je) {  // the module may be unloaded (jit_evict) only after this launch
+      if (!je->ev_last)
+        HIP_OR_FAIL(c, hipEventCreateWithFlags(&je->ev_last, hipEventDisableTiming));
+      HIP_OR_FAIL(c, hipEventRecord(je->ev_last, rstream));
+    }
+    c->last_set = set;
+    c->launches++;
+    return LT_OK;
+  }
   if (yf) {  // every pixel's flags are in (analyze + resolve): expand them into the planes
     const bool v4 = ((uintptr_t)out->spike % 4 == 0) && ((uintptr_t)out->vertex % 4 == 0) &&
                     out->stride % 4 == 0;
@@ -680,6 +847,10 @@ static int launch_tile(lt_ctx* c, const lt_params* prm, const lt_tile_in* in,
   }
   HIP_OR_FAIL(c, hipGetLastError());
   if (ep[1]) HIP_OR_FAIL(c, hipEventRecord(ep[1]->stop, rstream));
+  if (ep[2]) {  // no expand stage: an empty interval
+    HIP_OR_FAIL(c, hipEventRecord(ep[2]->start, rstream));
+    HIP_OR_FAIL(c, hipEventRecord(ep[2]->stop, rstream));
+  }
   HIP_OR_FAIL(c, hipEventRecord(c->ev_resolved[set], rstream));
   if (je) {  // the module may be unloaded (jit_evict) only after this launch
     if (!je->ev_last)
@@ -833,7 +1004,8 @@ int lt_analyze_tiles_after(lt_ctx* c, const lt_scene* sc, const lt_params* prm, 
     if (rc != LT_OK) return rc;
     c->set_used[set] = true;
   }
-  HIP_OR_FAIL(c, hipEventRecord(c->ev_resolved[c->last_set], c->side));
+  // (the last tile's launch recorded ev_resolved after its last stage: the resolve kernels, or
+  // the trendline expand kernel on the expand stream)
   HIP_OR_FAIL(c, hipStreamWaitEvent(stream, c->ev_resolved[c->last_set], 0));
   return LT_OK;
 }
@@ -1001,6 +1173,7 @@ int lt_jit_source(const lt_scene* sc, const lt_params* prm, const lt_index_prog*
     sp.n_years = Y;
     sp.masked = masked != 0;
     sp.year_out = year_out != 0;
+    sp.tl_split = sp.year_out && !(getenv("LT_TL_SPLIT") && getenv("LT_TL_SPLIT")[0] == '0');
     sp.params = *prm;
     if (flags & LT_JIT_SRC_SCENE) sp.scene = &tmp;
   }

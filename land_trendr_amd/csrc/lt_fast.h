@@ -175,7 +175,8 @@ struct NoProbe {
 template <int MAXY, int RMAX, bool EXACT, class VT, class Probe = NoProbe>
 __device__ inline int analyze_fast(const DevScene& S_launch, const lt_params& P, const lt_tile_in& in,
                                    const lt_tile_out& out, const lsq_xf* __restrict__ xtab,
-                                   uint64_t* __restrict__ yflags, int64_t p, bool live, int lane,
+                                   uint64_t* __restrict__ yflags, uint64_t* __restrict__ tl_bits,
+                                   double* __restrict__ tl_eqn, int64_t p, bool live, int lane,
                                    WaveLds<MAXY, VT, EXACT>& L,
                                    const Probe& probe = Probe()) {
   // the scene: constants of a JIT kernel specialised for it (lt_jit.h), else the launch's
@@ -1272,7 +1273,83 @@ __device__ inline int analyze_fast(const DevScene& S_launch, const lt_params& P,
     prev_fit = fit_vertex;
     prev_year = yr;
   };
-  if (year_out) {
+  // the compact trendline (launch-uniform; lt_abi.hip trendline_expand_kernel writes the per-year
+  // planes from it)
+#ifdef LT_SPEC_TL_SPLIT
+  constexpr bool tl_split = LT_SPEC_TL_SPLIT != 0;
+#else
+  const bool tl_split = tl_bits != nullptr;
+#endif
+  if (year_out && tl_split) {
+    // ---- compact trendline: the per-year planes are NOT written here. Lockstep over the vertex
+    // number q: one LAPACK-emulated fit per segment (vertices2eqns, utils.py:646-669), the
+    // fitted value at each vertex (eqns2fitted_points, utils.py:682-722: the closer of the left
+    // and the right eqn to the raw value, the left on a tie) for the rule offers, and per pixel
+    //   tl_eqn[q][p] = (m, b) of segment q (vertex q to vertex q+1), q < n_vertices - 1,
+    //   tl_bits[0][p] = present year slots (0: the reference raises for the pixel),
+    //   tl_bits[1][p] = spike flags by present index, tl_bits[2][p] = vertices by non-spike
+    //   index, tl_bits[3][p] = vertex q took the left eqn for its fitted value.
+    // trendline_expand_kernel then writes every year row from these, one thread per (pixel,
+    // year) with no store-then-load order inside a thread: here no year row is stored before a
+    // fit's x-set table loads (a load after stores waits for all of them on gfx950's one
+    // vector-memory counter: the year-major loop below spent ~2.7 ms of a 12.4 ms c5 launch
+    // there). The eqn of segment q is stored after segment q+1's table loads are
+    // issued, so those loads do not wait for it.
+    const bool emit = live && !deferred;
+    const bool good = emit && ok;
+    const uint64_t vm = good ? vmask : 0;
+    const int nv = __builtin_popcountll(vm);
+    const int nvmax = wave_max(nv);
+    uint64_t vrem = vm, left = 0;
+    double pm = 0.0, pb = 0.0;  // eqn of vertex q-1
+    double* const eq = tl_eqn;
+    const int64_t np = in.n_pix;
+    for (int q = 0; q < nvmax; q++) {
+      const bool act = q < nv;
+      const int ka = act ? __builtin_ctzll(vrem) : 0;
+      if (act) vrem &= vrem - 1;
+      const bool has_next = act && q + 1 < nv;
+      const int kb = has_next ? __builtin_ctzll(vrem) : ka;
+      double cm = pm, cb = pb;
+      if (__ballot(has_next)) {
+        double sm = 0.0, sbv = 0.0;
+        const int rc = lsq_fit_lockstep(
+            has_next, has_next ? kb - ka + 1 : 2,
+            [&](int k) { return (int)L.xn[(has_next ? ka : 0) + k][lane]; },
+            [&](int k) { return (double)L.ys[(has_next ? ka : 0) + k][lane]; }, xtab, sm, sbv);
+        if (has_next) {
+          if (rc < 0) status |= LT_ST_NUMERIC;
+          cm = sm;
+          cb = sbv;
+          // one 16-byte store per lane, rows [q][p] coalesced across the wave
+          typedef double d2 __attribute__((ext_vector_type(2)));
+          d2 v;
+          v.x = cm;
+          v.y = cb;
+          __builtin_nontemporal_store(v, (d2*)(eq + 2 * ((int64_t)q * np + p)));
+        }
+      }
+      const double raw_v = act ? (double)L.ys[ka][lane] : 0.0;
+      const double x = act ? (double)L.xn[ka][lane] : 0.0;  // the vertex's year offset
+      double fit_vertex = (cm * x) + cb;
+      if (q > 0 && !(pm == cm && pb == cb)) {
+        const double fl = (pm * x) + pb;
+        if (__builtin_fabs(fl - raw_v) <= __builtin_fabs(fit_vertex - raw_v)) {
+          fit_vertex = fl;
+          left |= 1ull << q;
+        }
+      }
+      if (act) offer_rules(q, y0 + L.xn[ka][lane], fit_vertex);
+      pm = cm;
+      pb = cb;
+    }
+    if (emit) {
+      __builtin_nontemporal_store(good ? pres : 0ull, tl_bits + p);
+      __builtin_nontemporal_store(spike, tl_bits + np + p);
+      __builtin_nontemporal_store(vm, tl_bits + 2 * np + p);
+      __builtin_nontemporal_store(left, tl_bits + 3 * np + p);
+    }
+  } else if (year_out) {
     // Year-major: every year slot is one wave-uniform step and each per-year plane is written
     // one coalesced row at a time (lane l -> pixel p, all lanes the same year). A lane reaching
     // a vertex that has a next vertex needs that segment's fit (lanes without a next vertex reuse

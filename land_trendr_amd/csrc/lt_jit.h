@@ -207,7 +207,7 @@ inline const char* series_type(int out_type, int n_rules) {
 struct Spec {
   bool on = false;
   int n_years = 0;
-  bool masked = false, year_out = false;
+  bool masked = false, year_out = false, tl_split = false;
   lt_params params{};
   const lt::DevScene* scene = nullptr;  // the scene's tables as constants (LT_SPEC_SCENE)
 };
@@ -265,7 +265,8 @@ inline uint64_t spec_key(const lt_index_prog& P, int maxy, int rmax, const char*
   }
   const int inst[3] = {maxy, rmax, (int)strlen(vt)};
   h = fnv1a_bytes(inst, sizeof inst, fnv1a(std::string(vt), h));
-  const int flags[4] = {sp.on ? 1 : 0, sp.n_years, sp.masked ? 1 : 0, sp.year_out ? 1 : 0};
+  const int flags[5] = {sp.on ? 1 : 0, sp.n_years, sp.masked ? 1 : 0, sp.year_out ? 1 : 0,
+                        sp.tl_split ? 1 : 0};
   h = fnv1a_bytes(flags, sizeof flags, h);
   if (sp.on) {
     const lt_params& Q = sp.params;
@@ -328,10 +329,10 @@ inline std::string source(const lt_index_prog& P, int maxy, int rmax, const char
     char d[512];
     snprintf(d, sizeof d,
              "#include \"lt_abi.h\"\n#define LT_SPEC_Y %d\n#define LT_SPEC_MASKED %d\n"
-             "#define LT_SPEC_YEAR_OUT %d\n#define LT_SPEC_NRULES %d\n#define LT_SPEC_PRE_MODE %d\n"
-             "#define LT_SPEC_LINE_COST %a\n",
-             sp.n_years, sp.masked ? 1 : 0, sp.year_out ? 1 : 0, Q.n_rules, Q.pre_threshold_mode,
-             Q.line_cost);
+             "#define LT_SPEC_YEAR_OUT %d\n#define LT_SPEC_TL_SPLIT %d\n#define LT_SPEC_NRULES %d\n"
+             "#define LT_SPEC_PRE_MODE %d\n#define LT_SPEC_LINE_COST %a\n",
+             sp.n_years, sp.masked ? 1 : 0, sp.year_out ? 1 : 0, sp.tl_split ? 1 : 0, Q.n_rules,
+             Q.pre_threshold_mode, Q.line_cost);
     src += d;
     src += "__device__ constexpr lt_rule lt_spec_rules[" +
            std::to_string(Q.n_rules > 0 ? Q.n_rules : 1) + "] = {";

@@ -66,7 +66,8 @@ inline SeriesKind series_kind(const TileLaunch& l) {
 inline dim3 tile_grid(const TileLaunch& l) { return dim3((unsigned)((l.in->n_pix + 63) / 64)); }
 
 inline KernelArgs kernel_args(const TileLaunch& l, int64_t* defer, unsigned long long* counters) {
-  return KernelArgs{l.scene, *l.params, *l.in, *l.out, l.xtab, defer, counters, l.yflags};
+  return KernelArgs{l.scene, *l.params, *l.in, *l.out, l.xtab, defer, counters, l.yflags,
+                    l.tl_bits, l.tl_eqn};
 }
 
 template <int MAXY, int RMAX, int WAVES, class Probe>

@@ -37,6 +37,8 @@ struct KernelArgs {
   int64_t* defer;
   unsigned long long* n_defer;  // analyze: [0]/[2] list counts; resolve: its counters
   uint64_t* yflags;
+  uint64_t* tl_bits;  // the compact trendline (lt_fast.h tl_split), or null
+  double* tl_eqn;
 };
 
 __device__ inline const KernelArgs& args() {
@@ -57,8 +59,9 @@ __device__ inline void analyze_body() {
   const int64_t p = (int64_t)blockIdx.x * 64 + lane;
   const int64_t n_pix = K.in.n_pix;
   const bool live = p < n_pix;
-  const int d = analyze_fast<MAXY, RMAX, false, VT>(*K.S, K.P, K.in, K.out, K.xtab, K.yflags, p,
-                                                    live, lane, L, Probe{});
+  const int d = analyze_fast<MAXY, RMAX, false, VT>(*K.S, K.P, K.in, K.out, K.xtab, K.yflags,
+                                                    K.tl_bits, K.tl_eqn, p, live, lane, L,
+                                                    Probe{});
   // two lists: [0, n_pix) for the binary32 resolve, [n_pix, 2 n_pix) for the binary64 one;
   // counters [0] / [2] count them (wave-aggregated atomics)
   const KernelArgs& K2 = args();
@@ -94,7 +97,8 @@ __device__ inline void resolve_body() {
     const bool live = lane < G && k < n;
     const KernelArgs& Kk = args();
     analyze_fast<MAXY, RMAX, true, VT>(*Kk.S, Kk.P, Kk.in, Kk.out, Kk.xtab, Kk.yflags,
-                                       live ? Kk.defer[k] : 0, live, lane, L);
+                                       Kk.tl_bits, Kk.tl_eqn, live ? Kk.defer[k] : 0, live, lane,
+                                       L);
   }
 }
 

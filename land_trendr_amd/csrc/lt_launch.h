@@ -25,6 +25,8 @@ struct TileLaunch {
   int n_years;                   // Y
   int device;
   hipStream_t stream;
+  uint64_t* tl_bits = nullptr;   // the compact trendline ([4][n_pix] words), or null
+  double* tl_eqn = nullptr;      // its segment eqns ([Y-1][n_pix] (m, b) pairs)
 };
 
 // Stage 1: the analyze kernel over every pixel of the tile, on l.stream.

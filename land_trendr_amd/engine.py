@@ -303,10 +303,10 @@ class Engine:
         self._check(self.lib.lt_ctx_set_timing(self.ctx, 1 if enable else 0), 'set_timing')
 
     def stage_ms(self):
-        ms = (ctypes.c_double * 2)()
+        ms = (ctypes.c_double * 3)()
         n = ctypes.c_int64()
-        self._check(self.lib.lt_ctx_stage_ms(self.ctx, ms, 2, ctypes.byref(n)), 'stage_ms')
-        return {'analyze': ms[0], 'resolve': ms[1], 'launches': n.value}
+        self._check(self.lib.lt_ctx_stage_ms(self.ctx, ms, 3, ctypes.byref(n)), 'stage_ms')
+        return {'analyze': ms[0], 'resolve': ms[1], 'expand': ms[2], 'launches': n.value}
 
     def last_deferred(self):
         n = ctypes.c_int64()
