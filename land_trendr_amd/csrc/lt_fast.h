@@ -1081,7 +1081,8 @@ __device__ inline int analyze_fast(const DevScene& S_launch, const lt_params& P,
         const double D = (double)dmul24(m, sxx, sx);
         const double t1 = __builtin_fma(md, syy, -(sy * sy));
         const double N1 = __builtin_fma(md, sxy, -((double)sx * sy));
-        return kZero * syy < 0x1p-54 * c && sse_exact_zero(t1, D, N1);
+        // (wx0: the year offset of point j, the segment's largest)
+        return zero_bound(wx0) * syy < 0x1p-54 * c && sse_exact_zero(t1, D, N1);
       };
       // a start of >= 3 points: a zero-residual start (v recomputed as the reference's
       // fl(c + OPTa[i])) or an interval candidate that starts a new base if it wins

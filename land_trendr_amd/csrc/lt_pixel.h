@@ -346,8 +346,14 @@ __host__ __device__ inline double dp_start_bound(double e, double opta, double e
 // and kZero * Syy < 2^-54 c, e lies below half an ulp of c, so fl(e + c) = c: the start is worth
 // fl(c + OPT[i]) like a 1-2 point start, and is exact whenever OPT[i] is.
 // kZero bounds the emulated residual of exactly collinear segments: tests/test_screening.py
-// measures at most 2^-93 Syy (m <= 64, int16 values, gapped x sets).
+// measures at most 2^-93 Syy (m <= 64, int16 values, gapped x sets). The a-priori bound (DESIGN.md
+// § Screening bounds, tests/test_screening_bounds.py) is eta^2 Syy with eta growing with the
+// segment's largest year offset X: at most 2^-84 for X <= 63, but up to 2^-80.2 for X <= 255
+// (year spans up to 255 are accepted, lt_abi.hip), so segments reaching past offset 63 use
+// kZeroWide instead (zero_bound).
 constexpr double kZero = 0x1p-80;
+constexpr double kZeroWide = 0x1p-74;
+__host__ __device__ inline double zero_bound(int x_max) { return x_max <= 63 ? kZero : kZeroWide; }
 
 // t1 * D == N1^2 exactly (the closed form's numerator m*D*SSE is 0): t1, D and N1 are exact
 // integers in binary64 when the values are integers of int16 range (|Sy| < 2^21, Syy < 2^36),
@@ -514,7 +520,7 @@ __host__ __device__ inline bool dp_lazy(int n, const uint8_t* xs, const double* 
         e = (t1 - N1 * N1 / D) / md;
         if (e < 0.0) e = 0.0;
         ws = kScreen * Syy;
-        if (zero_ok && intdata && e <= ws && kZero * Syy < 0x1p-54 * c &&
+        if (zero_ok && intdata && e <= ws && zero_bound(xs[j]) * Syy < 0x1p-54 * c &&
             sse_exact_zero(t1, D, N1)) {
           zr = true;
           e = 0.0;
