@@ -92,70 +92,84 @@ __global__ __launch_bounds__(kBlock) void year_flags_kernel(const uint64_t* __re
 
 // The per-year trendline planes from the compact trendline the analyze / resolve stages leave
 // (lt_fast.h tl_split): eqns2fitted_points (utils.py:682-722) and the TrendlinePoint fields
-// (classes.py:67-116) of year slot y = blockIdx.y for one pixel per thread. Everything follows
-// from the pixel's four words — present years P0 (0: the reference raises), spike flags by present
-// index, vertices by non-spike index, the left-eqn choice by vertex number — and at most two
-// segment eqns:
+// (classes.py:67-116). Everything follows from the pixel's four words — present years P0 (0: the
+// reference raises), spike flags by present index, vertices by non-spike index, the left-eqn
+// choice by vertex number — and the segment eqns:
 //   t = present index of slot y, spike = bit t, k = its non-spike index, vertex = bit k;
 //   passed = vertices at or before the point; the current eqn is segment passed-1, or, past the
 //   last vertex (whose eqn is its left segment's, utils.py:662), segment n_vertices-2;
 //   val_fit = m x + b of the current eqn (x = year offset from the first present year, no FMA),
 //   or of the previous one at an interior vertex that took the left eqn;
 //   fit_m / fit_b = the eqn used, right_m / right_b = the current one; NaN for absent years.
-// Exactly the values of the year-major loop (lt_fast.h, tl_split off), which it replaces. Each
-// thread only loads, then stores: no store-then-load order inside a thread. Rows: 256 pixels of
-// one year per block, so every plane row is written in 2 KB (binary64) / 256 B (u8) runs; the
-// Y blocks of one pixel range are consecutive (block b: year b % Y, pixels b / Y), so its words
-// and eqns are read from HBM once and from L2 by the other years (year-major blocks re-read the
-// whole tile's words per year: 11.5 ms per 16.8 Mpx c5 tile, profiles/r05_run4).
+// Exactly the values of the year-major loop (lt_fast.h, tl_split off), which it replaces.
+// One thread per (pixel, chunk of kYC year slots): its four words, then every eqn the chunk's
+// years use (all loads in flight together), then the chunk's rows (stores only: no store before
+// a load in a thread). A thread per (pixel, year) waited out three dependent load round trips per
+// seven stores: 9.3 ms per 16.8 Mpx c5 tile, 3.0 TB/s (profiles/r05_run5). Blocks: 256 pixels of
+// one chunk, the chunks of a pixel range consecutive (its words and eqns then come from L2).
+constexpr int kYC = 8;
 __global__ __launch_bounds__(kBlock) void trendline_expand_kernel(
     const lt::DevScene* __restrict__ S, const uint64_t* __restrict__ bits,
     const double* __restrict__ eqn, int64_t n, int Y, const lt_tile_out out) {
-  const int y = (int)(blockIdx.x % (unsigned)Y);
-  const int64_t p = (int64_t)(blockIdx.x / (unsigned)Y) * kBlock + threadIdx.x;
+  const int nch = (Y + kYC - 1) / kYC;
+  const int ya = (int)(blockIdx.x % (unsigned)nch) * kYC;
+  const int64_t p = (int64_t)(blockIdx.x / (unsigned)nch) * kBlock + threadIdx.x;
   if (p >= n) return;
-  const uint64_t P0 = bits[p];
-  const double nan = __builtin_nan("");
-  double fv = nan, fm = nan, fb = nan, rm = nan, rb = nan;
-  uint8_t sp = 0, vx = 0;
-  if ((P0 >> y) & 1) {
-    const uint64_t SP = bits[n + p], VM = bits[2 * n + p], LB = bits[3 * n + p];
+  const uint64_t P0 = bits[p], SP = bits[n + p], VM = bits[2 * n + p], LB = bits[3 * n + p];
+  const int nvt = __builtin_popcountll(VM);
+  typedef double d2 __attribute__((ext_vector_type(2)));
+  d2 cur[kYC], prv[kYC];
+  // (1) every eqn the chunk needs, loads issued together
+#pragma unroll
+  for (int j = 0; j < kYC; j++) {
+    const int y = ya + j;
+    cur[j] = d2{0.0, 0.0};
+    prv[j] = d2{0.0, 0.0};
+    if (y >= Y || !((P0 >> y) & 1)) continue;
     const int t = __builtin_popcountll(P0 & ((1ull << y) - 1));  // y <= 63
-    sp = (uint8_t)((SP >> t) & 1);
+    const bool sp = (SP >> t) & 1;
     const int k = t - __builtin_popcountll(SP & ((1ull << t) - 1));
-    vx = (uint8_t)(!sp && ((VM >> k) & 1));
-    const int nvt = __builtin_popcountll(VM);
+    const bool vx = !sp && ((VM >> k) & 1);
     const uint64_t upto = sp ? ((1ull << k) - 1) : (k >= 63 ? ~0ull : ((2ull << k) - 1));
     const int qc = __builtin_popcountll(VM & upto) - 1;  // the last vertex at or before the point
     const int e = qc + 1 >= nvt ? nvt - 2 : qc;
-    double cm = 0.0, cb = 0.0;
-    typedef double d2 __attribute__((ext_vector_type(2)));
-    if (e >= 0) {
-      const d2 v = *(const d2*)(eqn + 2 * ((int64_t)e * n + p));
-      cm = v.x;
-      cb = v.y;
-    }
-    const double x = (double)(S->year[y] - S->year[__builtin_ctzll(P0)]);
-    fv = (cm * x) + cb;
-    fm = cm;
-    fb = cb;
-    rm = cm;
-    rb = cb;
-    if (vx && qc > 0 && qc < nvt - 1 && ((LB >> qc) & 1)) {
-      const d2 v = *(const d2*)(eqn + 2 * ((int64_t)(qc - 1) * n + p));
-      fv = (v.x * x) + v.y;
-      fm = v.x;
-      fb = v.y;
-    }
+    if (e >= 0) cur[j] = *(const d2*)(eqn + 2 * ((int64_t)e * n + p));
+    if (vx && qc > 0 && qc < nvt - 1 && ((LB >> qc) & 1))
+      prv[j] = *(const d2*)(eqn + 2 * ((int64_t)(qc - 1) * n + p));
   }
-  const int64_t o = (int64_t)y * out.stride + p;
-  if (out.val_fit) __builtin_nontemporal_store(fv, out.val_fit + o);
-  if (out.fit_m) __builtin_nontemporal_store(fm, out.fit_m + o);
-  if (out.fit_b) __builtin_nontemporal_store(fb, out.fit_b + o);
-  if (out.right_m) __builtin_nontemporal_store(rm, out.right_m + o);
-  if (out.right_b) __builtin_nontemporal_store(rb, out.right_b + o);
-  if (out.spike) out.spike[o] = sp;
-  if (out.vertex) out.vertex[o] = vx;
+  // (2) the rows
+  const double nan = __builtin_nan("");
+  const int32_t y0 = P0 ? S->year[__builtin_ctzll(P0)] : 0;
+#pragma unroll
+  for (int j = 0; j < kYC; j++) {
+    const int y = ya + j;
+    if (y >= Y) break;
+    double fv = nan, fm = nan, fb = nan, rm = nan, rb = nan;
+    uint8_t sp = 0, vx = 0;
+    if ((P0 >> y) & 1) {
+      const int t = __builtin_popcountll(P0 & ((1ull << y) - 1));
+      sp = (uint8_t)((SP >> t) & 1);
+      const int k = t - __builtin_popcountll(SP & ((1ull << t) - 1));
+      vx = (uint8_t)(!sp && ((VM >> k) & 1));
+      const uint64_t upto = sp ? ((1ull << k) - 1) : (k >= 63 ? ~0ull : ((2ull << k) - 1));
+      const int qc = __builtin_popcountll(VM & upto) - 1;
+      const double x = (double)(S->year[y] - y0);
+      rm = cur[j].x;
+      rb = cur[j].y;
+      const bool lft = vx && qc > 0 && qc < nvt - 1 && ((LB >> qc) & 1);
+      fm = lft ? prv[j].x : rm;
+      fb = lft ? prv[j].y : rb;
+      fv = (fm * x) + fb;
+    }
+    const int64_t o = (int64_t)y * out.stride + p;
+    if (out.val_fit) __builtin_nontemporal_store(fv, out.val_fit + o);
+    if (out.fit_m) __builtin_nontemporal_store(fm, out.fit_m + o);
+    if (out.fit_b) __builtin_nontemporal_store(fb, out.fit_b + o);
+    if (out.right_m) __builtin_nontemporal_store(rm, out.right_m + o);
+    if (out.right_b) __builtin_nontemporal_store(rb, out.right_b + o);
+    if (out.spike) out.spike[o] = sp;
+    if (out.vertex) out.vertex[o] = vx;
+  }
 }
 
 struct YearArg {
@@ -815,7 +829,7 @@ static int launch_tile(lt_ctx* c, const lt_params* prm, const lt_tile_in* in,
     HIP_OR_FAIL(c, hipStreamWaitEvent(c->xstream, c->ev_rdone[set], 0));
     if (ep[2]) HIP_OR_FAIL(c, hipEventRecord(ep[2]->start, c->xstream));
     if (Y > 0) {
-      const int64_t nb = (in->n_pix + kBlock - 1) / kBlock * Y;
+      const int64_t nb = (in->n_pix + kBlock - 1) / kBlock * ((Y + kYC - 1) / kYC);
       if (nb > 0x7fffffff) return fail(c, LT_ERR_LIMIT, "tile too large for the expand grid%s");
       hipLaunchKernelGGL(trendline_expand_kernel, dim3((unsigned)nb), dim3(kBlock), 0,
                          c->xstream, c->d_scene, l.tl_bits, l.tl_eqn, in->n_pix, Y, *out);

@@ -1545,6 +1545,8 @@ __device__ inline int analyze_fast(const DevScene& S_launch, const lt_params& P,
           cm = N1 * r;
           cb = __builtin_fma(-cm, (double)Sx, Sy) * rm;
           csc = __builtin_fma(__builtin_fabs(cm), 64.0, __builtin_fabs(cb)) + ymx;
+          // a segment reaching past year offset 63: kFitWide (lt_pixel.h fit_width)
+          csc *= fit_width_factor(L.xn[kb][lane]);
         }
       }
       // the fitted value at vertex q (eqns2fitted_points: the closer of the left and right eqn)

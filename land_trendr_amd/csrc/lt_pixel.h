@@ -160,8 +160,12 @@ struct RuleCands {
 // Half-width factor of a closed-form vertex fit against the reference's (emulated dgelsd) one:
 // |fitted value - reference fitted value| <= kFitW * (|slope| * 64 + |intercept| + max|y|) at any
 // year offset x < 64. tests/test_screening.py measures the emulated dgelsd and the kernel's closed
-// form against the exact rational fit over adversarial segments and requires a 2^10 margin.
+// form against the exact rational fit over adversarial segments and requires a 2^10 margin. The
+// a-priori bound (DESIGN.md § Screening bounds, tests/test_screening_bounds.py) is 2^-35.4 of the
+// scale for segments within offsets 0..63, but grows with the conditioning of [1, x] past that (a
+// short segment at offsets near 255: 2^-31.4): such segments use 16 kFitW (fit_width_factor).
 constexpr double kFitW = 0x1p-32;
+__host__ __device__ inline double fit_width_factor(int x_max) { return x_max <= 63 ? 1.0 : 16.0; }
 
 // change_labeling state for all rules (classes.py:213-230 winner bookkeeping).
 struct RuleState {
