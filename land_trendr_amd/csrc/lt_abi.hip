@@ -298,7 +298,11 @@ struct lt_ctx {
   hipEvent_t ev_rdone[kSets] = {};  // a tile's resolve kernels done (the expand kernel waits)
   hipEvent_t ev_xdone = nullptr;    // the last expand kernel queued
   bool x_used = false;
-  bool tl_split = true;  // LT_TL_SPLIT at creation
+  // LT_TL_SPLIT=1 at creation: per-year planes through the compact trendline and the expand
+  // kernel. Off by default: measured slower on c5 (899 vs 1228 Mpx/s, profiles/r05_run6): the
+  // analyze kernel drops from 12.3 to 9.0-9.3 ms per 16.8 Mpx tile, but the expand kernel takes
+  // 8.1 ms alone (28 GB of rows at 3.5 TB/s) and gets CU slots only between analyze launches
+  bool tl_split = false;
 };
 
 static int fail(lt_ctx* c, int code, const char* fmt, const char* detail = "") {
@@ -353,7 +357,7 @@ int lt_ctx_create(int device, lt_ctx** out) {
     if (atoi(e) >= 1) c->jit_max_modules = atoi(e);
   if (const char* e = getenv("LT_JIT_SCENE_MAX"))
     if (atoi(e) >= 0) c->jit_scene_max = atoi(e);
-  if (const char* e = getenv("LT_TL_SPLIT")) c->tl_split = e[0] != '0';
+  if (const char* e = getenv("LT_TL_SPLIT")) c->tl_split = e[0] == '1';
   hipError_t e = hipSetDevice(device);
   if (e == hipSuccess) e = hipHostMalloc((void**)&c->h_scene, sizeof(lt::DevScene));
   if (e == hipSuccess) e = hipMalloc((void**)&c->d_scene, sizeof(lt::DevScene));
@@ -487,8 +491,8 @@ static int check_tile(lt_ctx* c, const lt_tile_in* in, const lt_tile_out* out) {
 }
 
 // Per-year planes with the compact trendline (lt_fast.h tl_split, trendline_expand_kernel):
-// every launch asking for any of them, unless the context was created with LT_TL_SPLIT=0 (A/B
-// runs and tests: the year-major loop)
+// every launch asking for any of them when the context was created with LT_TL_SPLIT=1 (else the
+// year-major loop writes them)
 static bool tl_split_launch(const lt_ctx* c, const lt_tile_out* o) {
   return c->tl_split && (o->val_fit || o->fit_m || o->fit_b || o->right_m || o->right_b ||
                          o->spike || o->vertex);
@@ -1189,7 +1193,7 @@ int lt_jit_source(const lt_scene* sc, const lt_params* prm, const lt_index_prog*
     sp.n_years = Y;
     sp.masked = masked != 0;
     sp.year_out = year_out != 0;
-    sp.tl_split = sp.year_out && !(getenv("LT_TL_SPLIT") && getenv("LT_TL_SPLIT")[0] == '0');
+    sp.tl_split = sp.year_out && getenv("LT_TL_SPLIT") && getenv("LT_TL_SPLIT")[0] == '1';
     sp.params = *prm;
     if (flags & LT_JIT_SRC_SCENE) sp.scene = &tmp;
   }
