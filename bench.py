@@ -334,6 +334,9 @@ def main():
                          'compared with every plane they wrote (0: skip; A/B timing runs only)')
     ap.add_argument('--serial-load', action='store_true',
                     help='run the index_eqn kernels on the analyze stream (no load stream)')
+    ap.add_argument('--tiled-steps', type=int, default=3,
+                    help='N = 1, labels-only configs: steps of the N > 1 tiling (16.8 Mpx tiles) '
+                         'timed after the main ones (0: skip)')
     ap.add_argument('--index-eqn', default='B1 - B2',
                     help='attribution runs: another index_eqn over the same two int16 bands, e.g. '
                          '"(B1 - B2) * 2 / 2" (the same values through a program that is not a '
@@ -508,6 +511,36 @@ def main():
                            'rasters' + (' and of every per-year trendline plane per tile '
                                         '(TrendlineStream)' if cfg['trendline'] else '')}
 
+    # N = 1: the rate of the N > 1 pipeline on this GPU (16.8 Mpx tiles of the scene in one call,
+    # per-tile completion events as the label exchange uses them), so the driver's N = 1 point and
+    # its N > 1 points can be compared pipeline for pipeline
+    tiled = None
+    if world == 1 and not mosaic_cfg and mosaic.tile > (1 << 24) and args.tiled_steps > 0:
+        m3 = Mosaic([P], 1 << 24, 1, 0, 'by_scene')
+        items3 = mosaic_inputs(m3, cfg['years'], cfg['k'][0], cfg['k'][1], cfg['mask'],
+                               cfg['seed'], dev, TARGET,
+                               band_layout=os.environ.get('LT_BAND_LAYOUT',
+                                                          'pixel' if fused else 'planar'),
+                               mask_format=os.environ.get('LT_MASK_FORMAT', 'bits'))
+        r3 = MosaicRunner(eng, m3, params, items3, fields, index_fn, None, exchange_fields=(),
+                          load_stream=not args.serial_load, group=args.group)
+        r3.gathering = True  # the N > 1 call pattern: completion events, no per-call join
+        r3.prepare_jit(wait=True)
+        r3.step()
+        torch.cuda.synchronize()
+        t3 = time.perf_counter()
+        for _ in range(args.tiled_steps):
+            r3.step()
+        torch.cuda.synchronize()
+        dt3 = time.perf_counter() - t3
+        tiled = {'tile_pixels': m3.tile, 'tiles': len(m3.tiles), 'steps': args.tiled_steps,
+                 'value': round(P * args.tiled_steps / dt3 / 1e6, 3), 'unit': 'Mpixels/s',
+                 'ms_per_step': round(dt3 / args.tiled_steps * 1e3, 3),
+                 'pipeline': 'the N > 1 one: 16.8 Mpx tiles, one lt_analyze_tiles_ev call per '
+                             'scene with per-tile completion events (no exchange at N = 1)'}
+        del r3, items3
+        torch.cuda.empty_cache()
+
     total_px = mosaic.n_pix * args.steps
     value = total_px / elapsed / 1e6
     n_launch = max(1, stages['launches'])
@@ -634,6 +667,8 @@ def main():
                           'deferred_pixels_last_tile': n_deferred_last,
                           'last_tile_pixels': items[-1].tile.n},
         'end_to_end': e2e,
+        'n_gt_1_tiling': None if tiled is None else dict(
+            tiled, ratio_to_value=round(tiled['value'] / value, 4)),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res['cpu_baseline'] = cpu_baseline(cfg, args.cpu_seconds)

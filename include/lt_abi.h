@@ -307,6 +307,15 @@ int lt_analyze_tiles_after(lt_ctx* ctx, const lt_scene* scene, const lt_params* 
                            int n_tiles, const lt_tile_in* ins, const lt_tile_out* outs,
                            void* const* ready, void* stream);
 
+/* lt_analyze_tiles_after that also records, for every tile t with done[t] != NULL, the caller's
+ * hipEvent_t done[t] once every output of tile t is complete (`done` itself may be NULL), and
+ * with join == 0 returns WITHOUT making `stream` wait for the tiles' last stages: the caller then
+ * orders later work on the done events (ABI 7; a multi-GPU runner posts tile t's label send after
+ * done[t], so tile t's resolve stage keeps running beside tile t+1's analyze kernel). */
+int lt_analyze_tiles_ev(lt_ctx* ctx, const lt_scene* scene, const lt_params* params, int n_tiles,
+                        const lt_tile_in* ins, const lt_tile_out* outs, void* const* ready,
+                        void* const* done, int32_t join, void* stream);
+
 /* change_labeling alone (utils.py:795-820) on trendlines already in device memory. Writes the
  * rule planes of `out` and out->status (only LT_ST_PRE_THRESHOLD_ATTR can be set). */
 int lt_label_tile(lt_ctx* ctx, const lt_label_in* in, const lt_params* params,

@@ -172,7 +172,7 @@ EXPORTS = ['lt_abi_version', 'lt_ctx_create', 'lt_ctx_destroy', 'lt_last_error',
            'lt_ctx_last_deferred', 'lt_index_codegen', 'lt_index_compile', 'lt_index_apply',
            'lt_settings_compile', 'lt_raster_assemble', 'lt_winner_presence',
            'lt_index_linearize', 'lt_ctx_set_jit_mode', 'lt_jit_prepare', 'lt_ctx_jit_stats',
-           'lt_jit_source']
+           'lt_jit_source', 'lt_analyze_tiles_ev']
 
 LT_JIT_SYNC, LT_JIT_ASYNC = 0, 1
 LT_JIT_SRC_SPEC, LT_JIT_SRC_SCENE = 1, 2
@@ -211,6 +211,10 @@ def load_lib(path=None):
     lib.lt_analyze_tiles_after.argtypes = [vp, ctypes.POINTER(LtScene), ctypes.POINTER(LtParams),
                                            ctypes.c_int, ctypes.POINTER(LtTileIn),
                                            ctypes.POINTER(LtTileOut), ctypes.POINTER(vp), vp]
+    lib.lt_analyze_tiles_ev.argtypes = [vp, ctypes.POINTER(LtScene), ctypes.POINTER(LtParams),
+                                        ctypes.c_int, ctypes.POINTER(LtTileIn),
+                                        ctypes.POINTER(LtTileOut), ctypes.POINTER(vp),
+                                        ctypes.POINTER(vp), ctypes.c_int32, vp]
     lib.lt_label_tile.argtypes = [vp, ctypes.POINTER(LtLabelIn), ctypes.POINTER(LtParams),
                                   ctypes.POINTER(LtTileOut), vp]
     lib.lt_ctx_set_timing.argtypes = [vp, ctypes.c_int]

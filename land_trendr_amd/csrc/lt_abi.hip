@@ -298,6 +298,7 @@ struct lt_ctx {
   hipEvent_t ev_rdone[kSets] = {};  // a tile's resolve kernels done (the expand kernel waits)
   hipEvent_t ev_xdone = nullptr;    // the last expand kernel queued
   bool x_used = false;
+  hipStream_t last_stage = nullptr;  // the stream of the last tile's last stage
   // LT_TL_SPLIT=1 at creation: per-year planes through the compact trendline and the expand
   // kernel. Off by default: measured slower on c5 (899 vs 1228 Mpx/s, profiles/r05_run6): the
   // analyze kernel drops from 12.3 to 9.0-9.3 ms per 16.8 Mpx tile, but the expand kernel takes
@@ -844,6 +845,7 @@ static int launch_tile(lt_ctx* c, const lt_params* prm, const lt_tile_in* in,
     HIP_OR_FAIL(c, hipEventRecord(c->ev_resolved[set], c->xstream));
     HIP_OR_FAIL(c, hipEventRecord(c->ev_xdone, c->xstream));
     c->x_used = true;
+    c->last_stage = c->xstream;
     if (je) {  // the module may be unloaded (jit_evict) only after this launch
       if (!je->ev_last)
         HIP_OR_FAIL(c, hipEventCreateWithFlags(&je->ev_last, hipEventDisableTiming));
@@ -872,6 +874,7 @@ static int launch_tile(lt_ctx* c, const lt_params* prm, const lt_tile_in* in,
     HIP_OR_FAIL(c, hipEventRecord(ep[2]->stop, rstream));
   }
   HIP_OR_FAIL(c, hipEventRecord(c->ev_resolved[set], rstream));
+  c->last_stage = rstream;
   if (je) {  // the module may be unloaded (jit_evict) only after this launch
     if (!je->ev_last)
       HIP_OR_FAIL(c, hipEventCreateWithFlags(&je->ev_last, hipEventDisableTiming));
@@ -940,6 +943,12 @@ int lt_analyze_tiles(lt_ctx* c, const lt_scene* sc, const lt_params* prm, int n_
 int lt_analyze_tiles_after(lt_ctx* c, const lt_scene* sc, const lt_params* prm, int n_tiles,
                            const lt_tile_in* ins, const lt_tile_out* outs, void* const* ready,
                            void* stream_) {
+  return lt_analyze_tiles_ev(c, sc, prm, n_tiles, ins, outs, ready, nullptr, 1, stream_);
+}
+
+int lt_analyze_tiles_ev(lt_ctx* c, const lt_scene* sc, const lt_params* prm, int n_tiles,
+                        const lt_tile_in* ins, const lt_tile_out* outs, void* const* ready,
+                        void* const* done, int32_t join, void* stream_) {
   if (!c) return LT_ERR_ARG;
   if (!sc || !prm || n_tiles < 0 || (n_tiles > 0 && (!ins || !outs)))
     return fail(c, LT_ERR_ARG, "null argument%s");
@@ -1023,7 +1032,11 @@ int lt_analyze_tiles_after(lt_ctx* c, const lt_scene* sc, const lt_params* prm, 
     const int rc = launch_tile(c, prm, &ins[t], &outs[t], Y, stream, c->side, set);
     if (rc != LT_OK) return rc;
     c->set_used[set] = true;
+    // the caller's per-tile event: after the tile's last stage (ev_resolved was just recorded on
+    // that stage's stream), e.g. for a label exchange that waits for this tile alone
+    if (done && done[t]) HIP_OR_FAIL(c, hipEventRecord((hipEvent_t)done[t], c->last_stage));
   }
+  if (!join) return LT_OK;
   // (the last tile's launch recorded ev_resolved after its last stage: the resolve kernels, or
   // the trendline expand kernel on the expand stream)
   HIP_OR_FAIL(c, hipStreamWaitEvent(stream, c->ev_resolved[c->last_set], 0));

@@ -140,13 +140,18 @@ class LabelExchange:
         self._recv_stream = (torch.cuda.Stream(self.device)
                              if self.is_writer and self.device.type == 'cuda' and not self._staged
                              else None)
+        # a sender's sends wait for their tile's completion event on a stream of their own
+        self._send_stream = (torch.cuda.Stream(self.device)
+                             if not self.is_writer and self.device.type == 'cuda' and
+                             not self._staged and mosaic.world > 1 else None)
         self._works = []
 
     def slab(self, tile):
         return self._slabs[tile.t]
 
-    def post(self, k):
-        """Round k: the k-th tile of every rank goes to the writer."""
+    def post(self, k, after=None):
+        """Round k: the k-th tile of every rank goes to the writer. after: an event (this rank's
+        tile k complete) the send waits for instead of the work queued on the current stream."""
         if self.m.world == 1:
             return
         d = self.dist
@@ -169,6 +174,8 @@ class LabelExchange:
             mine = self.m.mine
             if k < len(mine):
                 s = self._slabs[mine[k].t]
+                if self._staged and after is not None:  # the host copy below waits for it
+                    torch.cuda.current_stream(self.device).wait_event(after)
                 for f in self.fields:
                     src = s[f]
                     if self._staged:  # a blocking copy: after the kernels queued so far
@@ -178,6 +185,11 @@ class LabelExchange:
         if ops:
             if self._recv_stream is not None:
                 with torch.cuda.stream(self._recv_stream):
+                    self._works += d.batch_isend_irecv(ops)
+            elif after is not None and self._send_stream is not None:
+                # RCCL's stream waits for the send stream, which waits for this tile alone
+                with torch.cuda.stream(self._send_stream):
+                    self._send_stream.wait_event(after)
                     self._works += d.batch_isend_irecv(ops)
             else:
                 self._works += d.batch_isend_irecv(ops)

@@ -89,12 +89,15 @@ class Engine:
         return out
 
     def analyze_tiles(self, scene, params, tiles, fields=ALL_FIELDS, outs=None, stream=None,
-                      ready=None, lin=None, index=None):
+                      ready=None, lin=None, index=None, done=None, join=True):
         """analyze_tile over a list of (values, valid) tiles of one scene in one call
         (lt_analyze_tiles: tile t's resolve stage overlaps tile t+1's analyze stage). ready: None
         or one recorded torch.cuda.Event (or None) per tile, which that tile's analyze kernel
         waits on (lt_analyze_tiles_after: the load stage of later tiles may still be running on
         another stream). lin / index: as analyze_tile (every tile's values are then band planes).
+        done: None or one torch.cuda.Event (or None) per tile, recorded once every output of that
+        tile is complete; join=False: `stream` does not wait for the tiles' last stages
+        (lt_analyze_tiles_ev: the caller orders later work on the done events).
         Returns the list of output dicts; asynchronous on `stream`."""
         n = len(tiles)
         tins = (_abi.LtTileIn * max(n, 1))()
@@ -108,7 +111,19 @@ class Engine:
             res.append(o)
         sc = scene.to_c()
         st = stream if stream is not None else torch.cuda.current_stream(self.device)
-        if ready is None:
+        if done is not None or not join:
+            if done is not None and len(done) != n:
+                raise LtError('done needs one event (or None) per tile')
+            if ready is not None and len(ready) != n:
+                raise LtError('ready needs one event (or None) per tile')
+            evr = (ctypes.c_void_p * max(n, 1))(
+                *[e.cuda_event if e is not None else None for e in (ready or [None] * n)])
+            evd = (ctypes.c_void_p * max(n, 1))(
+                *[e.cuda_event if e is not None else None for e in (done or [None] * n)])
+            rc = self.lib.lt_analyze_tiles_ev(self.ctx, ctypes.byref(sc), ctypes.byref(params), n,
+                                              tins, touts, evr, evd, 1 if join else 0,
+                                              ctypes.c_void_p(st.cuda_stream))
+        elif ready is None:
             rc = self.lib.lt_analyze_tiles(self.ctx, ctypes.byref(sc), ctypes.byref(params), n,
                                            tins, touts, ctypes.c_void_p(st.cuda_stream))
         else:

@@ -86,8 +86,12 @@ class MosaicRunner:
             o = dict(self.exchange.slab(it.tile))
             o.update(shared[k % self.ring] if self.ring else planes())
             self.outs.append(o)
-        gathering = mosaic.world > 1 and bool(ex)
-        self.group = group if group > 0 else (1 if gathering else 1 << 30)
+        # with an exchange, every tile's label send waits for that tile's own completion event
+        # (lt_analyze_tiles_ev), not for the caller's stream: the tiles of a scene still share
+        # one call, so tile t's resolve stage keeps running beside tile t+1's analyze kernel
+        # (one call per tile, each joined to the stream before the next, serialised it)
+        self.gathering = mosaic.world > 1 and bool(ex)
+        self.group = group if group > 0 else 1 << 30
         if self.ring:
             self.group = 1
         has_bands = any(it.bands is not None for it in self.items)
@@ -116,6 +120,28 @@ class MosaicRunner:
                             if self.cuda and has_bands and load_stream and not self.fused
                             else None)
         self.index_events = []  # (start, stop) pairs of the timed steps' load kernels
+
+    def _done_events(self, n):
+        """Per-tile completion events for a call whose tiles' labels are exchanged (created by a
+        first record, so the library's record on its own stream is the one waited for), or None."""
+        if not (self.gathering and self.cuda):
+            return None
+        evs = [torch.cuda.Event() for _ in range(n)]
+        for e in evs:
+            e.record()
+        return evs
+
+    @staticmethod
+    def _ev_kw(done):
+        return {} if done is None else {'done': done, 'join': False}
+
+    def _join(self, pending):
+        """The current stream waits for every tile's completion: the step's outputs are complete
+        in stream order, as with joined calls."""
+        if pending:
+            cur = torch.cuda.current_stream(self.eng.device)
+            for e in pending:
+                cur.wait_event(e)
 
     def prepare_jit(self, wait=True):
         """Compile (wait) or start compiling the JIT module of every scene this rank's tiles
@@ -159,6 +185,7 @@ class MosaicRunner:
             return self._step_fused(after_tile, stage_in)
         main = torch.cuda.current_stream(eng.device) if self.cuda else None
         ready = [None] * len(self.items)
+        pending = []  # the tiles' completion events (gathering): the stream joins them at the end
         if self.load_stream is not None:  # the previous step's analyze kernels read the rasters
             self.load_stream.wait_stream(main)
         for k, it in enumerate(self.items):
@@ -189,20 +216,24 @@ class MosaicRunner:
             scene = self.items[g[0]].scene
             n = [self.items[k].tile.n for k in g]
             self._wait_ring(g[0])
+            done = self._done_events(len(g))
             eng.analyze_tiles(
                 scene, self.params, [(self.items[k].values, self.items[k].valid) for k in g],
                 self.fields, outs=[{f: x[..., :nk] for f, x in self.outs[k].items()}
                                    for k, nk in zip(g, n)],
-                ready=[ready[k] for k in g] if self.load_stream is not None else None)
-            for k in g:
-                self.exchange.post(k)
+                ready=[ready[k] for k in g] if self.load_stream is not None else None,
+                **self._ev_kw(done))
+            for j, k in enumerate(g):
+                self.exchange.post(k, after=done[j] if done is not None else None)
                 if after_tile is not None:
                     after_tile(k)
+            pending += done or []
         # rounds past this rank's own tiles: the writer still receives the tiles of ranks that
         # own more (unequal scenes under by_scene, or a writer other than rank 0); a sender has
         # nothing left to post
         for k in range(len(self.items), self.m.rounds):
             self.exchange.post(k)
+        self._join(pending)
         self.exchange.wait()
 
     def _step_fused(self, after_tile, stage_in):
@@ -213,6 +244,7 @@ class MosaicRunner:
         main = torch.cuda.current_stream(eng.device)
         groups = ([[k] for k in range(len(self.items))] if stage_in is not None
                   else list(self._groups()))
+        pending = []  # the tiles' completion events (gathering): the stream joins them at the end
         for g in groups:
             scene = self.items[g[0]].scene
             n = [self.items[k].tile.n for k in g]
@@ -224,20 +256,23 @@ class MosaicRunner:
                     ready = [ev_in]
                 tiles.append((bands, self.items[k].valid))
             self._wait_ring(g[0])
+            done = self._done_events(len(g))
             eng.analyze_tiles(
                 scene, self.params, tiles, self.fields,
                 outs=[{f: x[..., :nk] for f, x in self.outs[k].items()} for k, nk in zip(g, n)],
-                ready=ready, lin=self.lin, index=self.jit)
+                ready=ready, lin=self.lin, index=self.jit, **self._ev_kw(done))
             if stage_in is not None:
                 ev = torch.cuda.Event()
                 ev.record(main)
                 stage_in.consumed(g[0], ev)
-            for k in g:
-                self.exchange.post(k)
+            for j, k in enumerate(g):
+                self.exchange.post(k, after=done[j] if done is not None else None)
                 if after_tile is not None:
                     after_tile(k)
+            pending += done or []
         for k in range(len(self.items), self.m.rounds):
             self.exchange.post(k)
+        self._join(pending)
         self.exchange.wait()
 
     def _wait_ring(self, k):

@@ -1,0 +1,95 @@
+"""Does data movement make progress while the analyze kernel holds every CU? (VERDICT r04 item 4:
+the label exchange at N > 1 is RCCL point-to-point, which runs as kernels needing CU slots.)
+
+One GPU, bench.py's c2 launch (the JIT analyze kernel over one 49 Mpx scene), timed alone, then
+with a concurrent transfer on another stream started at the same moment:
+  * d2d_blit: a device-to-device copy of the c2 N = 8 writer ingress per step (7 x 49 Mpx x 20 B
+    = 6.9 GB), torch copy_ (HIP's blit kernel: needs CU slots, as RCCL's kernels do);
+  * d2h_sdma: a device-to-host copy into pinned memory (2 GB; the DMA engines, no CU slots).
+For each: the analyze step's time with the transfer beside it, the transfer's own time alone and
+when it completes relative to the step (an event on its stream). Prints one JSON object.
+"""
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+from land_trendr_amd.distributed import Mosaic  # noqa: E402
+from land_trendr_amd.engine import get_engine  # noqa: E402
+from land_trendr_amd.index_eqn import IndexProgram  # noqa: E402
+from land_trendr_amd.runner import MosaicRunner  # noqa: E402
+from land_trendr_amd.settings import compile_params  # noqa: E402
+from land_trendr_amd.synth import mosaic_inputs  # noqa: E402
+
+
+def main():
+    c = bench.CONFIGS['c2']
+    P = c['pixels']
+    dev = torch.device('cuda', 0)
+    eng = get_engine(0)
+    m = Mosaic([P], P, 1, 0, 'by_scene')
+    items = mosaic_inputs(m, c['years'], 1, 1, 0.0, c['seed'], dev, bench.TARGET)
+    params, _ = compile_params(c['line_cost'], c['rules'], c['mode'])
+    fn = eng.compile_index(IndexProgram('B1 - B2', band_dtype='int16'))
+    fields = ['status', 'matched', 'class_val', 'onset_year', 'duration', 'magnitude']
+    r = MosaicRunner(eng, m, params, items, fields, fn)
+    r.prepare_jit(wait=True)
+    r.step()
+    torch.cuda.synchronize()
+
+    def step_time(n=3):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(n):
+            r.step()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t) / n * 1e3
+
+    alone = step_time()
+    side = torch.cuda.Stream(dev)
+    ing = 7 * P * 20
+    src = torch.empty(ing, dtype=torch.uint8, device=dev)
+    dst = torch.empty_like(src)
+    dsrc = torch.empty(2 << 30, dtype=torch.uint8, device=dev)
+    hdst = torch.empty(2 << 30, dtype=torch.uint8, pin_memory=True)
+    res = {'analyze_step_alone_ms': round(alone, 3), 'pixels': P}
+    for name, (a, b) in {'d2d_blit': (dst, src), 'd2h_sdma': (hdst, dsrc)}.items():
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        with torch.cuda.stream(side):
+            e0.record()
+            a.copy_(b, non_blocking=True)
+            e1.record()
+        torch.cuda.synchronize()
+        t_alone = e0.elapsed_time(e1)
+        # both at once: the transfer queued first on its stream, the step right after
+        s0 = torch.cuda.Event(enable_timing=True)
+        x0, x1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        m0, m1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        s0.record()
+        side.wait_event(s0)
+        with torch.cuda.stream(side):
+            x0.record()
+            a.copy_(b, non_blocking=True)
+            x1.record()
+        m0.record()
+        r.step()
+        m1.record()
+        torch.cuda.synchronize()
+        res[name] = {'bytes': a.numel(), 'alone_ms': round(t_alone, 3),
+                     'alone_gbs': round(a.numel() / t_alone / 1e6, 1),
+                     'with_step': {'step_ms': round(m0.elapsed_time(m1), 3),
+                                   'transfer_done_after_ms': round(s0.elapsed_time(x1), 3),
+                                   'transfer_ms': round(x0.elapsed_time(x1), 3)}}
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == '__main__':
+    main()
