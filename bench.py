@@ -43,27 +43,33 @@ from land_trendr_amd.synth import make_scene, mosaic_inputs  # noqa: E402
 FP64_PEAK_TFLOPS = 78.6          # 256 CUs x 4 SIMDs x 16 lanes x 2 (FMA) x 2.4 GHz
 HBM_PEAK_GBS = 8000.0
 SIMDS, CLOCK_GHZ = 1024, 2.4
-VALU_PEAK_FILE = os.path.join('profiles', 'r04_valu_peak.json')
+VALU_PEAK_FILE = os.path.join('profiles', 'r05_valu_peak.json')
 
 
 def valu_peak():
     """The VALU issue peak the analyze kernel's roofline is priced against: measured on the box
-    by tools/valu_peak.hip (profiles/r04_valu_peak.json) — the chip's wave64 VALU instructions/s
+    by tools/valu_peak.hip (profiles/r05_valu_peak.json) — the chip's wave64 VALU instructions/s
     for a register-only stream of the c2 analyze kernel's instruction mix (PMC: 21 % FP64, 2 %
-    INT64, the rest 32-bit, half as many SALU) at the kernel's occupancy, 4 waves per SIMD.
-    Returns (G instructions/s, source, details)."""
+    INT64, the rest 32-bit, half as many SALU) at 8 waves per SIMD, the rate the SIMDs reach at
+    full occupancy (the 4-wave rate of the kernel's own occupancy hid the occupancy
+    cost; it is reported beside it). Returns (G instructions/s, source, details)."""
     try:
         with open(os.path.join(ROOT, VALU_PEAK_FILE)) as f:
             d = json.load(f)
         by = {(r['kind'], r['waves_per_simd']): r for r in d['results']}
-        mix = by[('mix_c2', 4)]
+        mix = by[('mix_c2', 8)]
         det = {k: round(by[(k, 4)]['cycles_per_valu_simd_nominal'], 3)
                for k in ('add_u32', 'cndmask_b32', 'cmp_gt_u32', 'fma_f32', 'add_f64', 'fma_f64',
-                         'mul_f64', 'rcp_f64', 'lshlrev_b64', 'mix_c2') if (k, 4) in by}
+                         'mul_f64', 'rcp_f64', 'lshlrev_b64', 'mix_c2', 'mov_b32', 'mov_b64',
+                         'cmp_cndmask_vcc', 'cmp_cnd2_vcc', 'cndmask_vcc_valu')
+               if (k, 4) in by}
+        det['mix_c2_at_4_waves_g_per_s'] = round(by[('mix_c2', 4)]['g_valu_per_s_chip'], 2)
         return mix['g_valu_per_s_chip'], VALU_PEAK_FILE, det
     except (OSError, ValueError, KeyError):
         # not measured: the 4-cycle-per-instruction model (an assumption, flagged in the line)
         return SIMDS * CLOCK_GHZ / 4, 'model: 4 cycles per wave64 VALU instruction', None
+
+
 TARGET = '2014-07-01'
 
 GD = [{'name': 'gd', 'val': 1, 'change_type': 'GD'}]
@@ -113,7 +119,7 @@ def pmc_summary(config, build):
     newest, whose '_matches_build' is then False and whose counters describe another build."""
     name = {'c4': 'c2'}.get(config, config)
     found = []
-    for rnd in ('r04', 'r03', 'r02'):  # newest first
+    for rnd in ('r05', 'r04', 'r03', 'r02'):  # newest first
         path = os.path.join(ROOT, 'profiles', '%s_pmc_%s.json' % (rnd, name))
         try:
             with open(path) as f:
@@ -602,15 +608,21 @@ def main():
                                    'to rank 0' % world) if mosaic_cfg else
                                   ('one scene per GPU (%d), labels sent to rank 0' % world)},
         # dominant kernel: analyze (>= 80 % of the GPU time), bound by VALU instruction issue —
-        # not HBM (85 B/px) and not FP64 throughput (21 % of its VALU work is FP64). achieved =
+        # not HBM (145 B/px on c2) and not FP64 throughput (23 % of its VALU work). achieved =
         # the VALU wave-instructions it issues per launch (PMC SQ_INSTS_VALU per pixel, committed
         # summary of this build) x pixels per launch / the launch's live HIP-event time; peak =
-        # the measured issue rate of a register-only stream of the same instruction mix at the
-        # same occupancy (tools/valu_peak.hip, profiles/r04_valu_peak.json)
+        # the measured issue rate of a register-only stream of the same instruction mix at full
+        # occupancy, 8 waves per SIMD (tools/valu_peak.hip, profiles/r05_valu_peak.json)
         'roofline': {'bound': 'valu-issue', 'achieved': r(achieved, 2), 'peak': round(peak_g, 2),
                      'unit': 'G VALU wave-instr/s',
                      'frac': r(achieved / peak_g if achieved else None),
-                     'peak_source': peak_src, 'cycles_per_valu_at_4_waves': peak_cyc,
+                     # against the same mix at the kernel's own occupancy (4 waves per SIMD,
+                     # 128 VGPRs): how close the kernel is to what its occupancy allows
+                     'frac_at_kernel_occupancy': r(
+                         achieved / peak_cyc['mix_c2_at_4_waves_g_per_s']
+                         if achieved and peak_cyc else None),
+                     'peak_source': peak_src, 'peak_waves_per_simd': 8,
+                     'cycles_per_valu_at_4_waves': peak_cyc,
                      'build': build, 'pmc_build': pmc.get('_build') if pmc else None,
                      'pmc_matches_build': bool(pmc and pmc['_matches_build']),
                      'pmc_refused': None if pmc_other is None else {

@@ -76,7 +76,17 @@ def build_hash():
         h.update(' '.join(ge.HIP_FLAGS).encode())
     except ImportError:
         pass
+    # switches that change the code the kernels run (JIT defines, specialisation, another
+    # library, override code objects, ...): a run under any of them is another build
+    for v in BUILD_ENV:
+        if os.environ.get(v):
+            h.update(('%s=%s\0' % (v, os.environ[v])).encode())
     return h.hexdigest()[:16]
+
+
+BUILD_ENV = ('LT_JIT_DEFINES', 'LT_JIT_SPEC', 'LT_JIT_LINEAR', 'LT_JIT_WAVES', 'LT_JIT_SCENE',
+             'LT_JIT_INDEX', 'LT_FUSED_INDEX', 'LT_TL_SPLIT', 'LT_JIT_OVERRIDE_DIR', 'LT_SRC_DIR',
+             'LT_HIP_LIB', 'LT_DEFER_SETS', 'LT_RESOLVE_PRIORITY', 'LT_EXPAND_PRIORITY')
 
 
 LT_LIN_MAX_BANDS = 4

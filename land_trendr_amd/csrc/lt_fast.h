@@ -47,6 +47,11 @@
 #ifndef LT_CERT_RULES
 #define LT_CERT_RULES 4
 #endif
+// labels-only certified path, pass B: fit only the eqns whose side pass A left undecided, in
+// lockstep slots (1), or all three eqns of every candidate (0)
+#ifndef LT_PASSB_SLOTS
+#define LT_PASSB_SLOTS 1
+#endif
 
 // Launch-uniform values a JIT kernel may be compiled for (lt_jit.h defines LT_SPEC_* for the
 // configuration it specialises; the precompiled kernels read them from the launch at run time):
@@ -1499,6 +1504,10 @@ __device__ inline int analyze_fast(const DevScene& S_launch, const lt_params& P,
     double am = 0.0, ab = 0.0, asc = 0.0;
     double fprev = 0.0, wprev = 0.0;  // fitted value of vertex q-1: center, half-width
     int32_t yprev = 0;
+    // interior vertices (by point index) whose fitted value certainly takes the left (CL) / the
+    // right (CR) eqn: the reference's choice, decided by the closed-form intervals (pass B then
+    // needs only that eqn's emulated fit there)
+    uint64_t CL = 0, CR = 0;
     auto add_pt = [&](int k, int& Sx, int& Sxx, double& Sy, double& Sxy, double& ymx)
                       __attribute__((always_inline)) {
       const int xi = L.xn[k][lane];
@@ -1561,10 +1570,13 @@ __device__ inline int analyze_fast(const DevScene& S_launch, const lt_params& P,
         if (dl + slack <= dr) {  // certainly the left eqn
           fv = fl;
           w = wl;
+          CL |= 1ull << ka;
         } else if (!(dr + slack < dl)) {  // either: the hull of both intervals
           const double lo = __builtin_fmin(fl - wl, fr - wr), hi = __builtin_fmax(fl + wl, fr + wr);
           fv = 0.5 * (lo + hi);
           w = 0.5 * (hi - lo) + 0x1p-50 * (__builtin_fabs(lo) + __builtin_fabs(hi));
+        } else {  // certainly the right eqn
+          CR |= 1ull << ka;
         }
       }
       const int32_t yr = y0 + (int32_t)x;
@@ -1607,30 +1619,59 @@ __device__ inline int analyze_fast(const DevScene& S_launch, const lt_params& P,
       const int kn = hasn ? __builtin_ctzll(above) : 0;               // vertex q+1
       // the reference's eqns (vertices2eqns, utils.py:646-669): e1 of segment q-1 (k1..kq),
       // e2 of segment q-2 (k2..k1), e3 of segment q (kq..kn)
-      double m1 = 0.0, b1 = 0.0, m2 = 0.0, b2 = 0.0, m3 = 0.0, b3 = 0.0;
-      auto fit = [&](bool on, int k0, int k9, double& sm, double& sb) __attribute__((always_inline)) {
+      // the fitted value at vertex q-1 takes e2 (left) or e1 (right), at vertex q e1 (left) or
+      // e3 (right): where pass A's intervals decided the side, only that eqn is fitted. A lane
+      // then needs at most two of the three (the third only at an undecided vertex), fitted in
+      // lockstep slots over the wave's largest count (three fixed steps: one always wasted).
+      // Each eqn is kept only as its values at the two vertices (fl1 / fr1 at vertex q-1, flq /
+      // frq at vertex q), all the choice needs: where two eqns are identical their values are,
+      // so the reference's "same eqn: the right one" shortcut gives the same value
+      // (LT_PASSB_SLOTS=0, A/B runs: the three eqns always, each fitted whenever a lane has it)
+      const bool slots = LT_PASSB_SLOTS != 0 && !infdata;
+      const bool cl1 = slots && has2 && ((CL >> k1) & 1), cr1 = slots && has2 && ((CR >> k1) & 1);
+      const bool clq = slots && hasn && ((CL >> kq) & 1), crq = slots && hasn && ((CR >> kq) & 1);
+      unsigned todo = (act && !(cl1 && crq) ? 1u : 0u) | (has2 && !cr1 ? 2u : 0u) |
+                      (hasn && !clq ? 4u : 0u);
+      const int nfit = wave_max(__builtin_popcount(todo));
+      double fl1 = 0.0, fr1 = 0.0, flq = 0.0, frq = 0.0;
+#pragma unroll
+      for (int sl = 0; sl < 3; sl++) {  // unrolled (a loop spilled 13-51 VGPRs across the fit)
+        if (sl >= nfit) break;           // wave-uniform
+        const bool on = todo != 0;
+        const int which = on ? __builtin_ctz(todo) : 0;  // 0: e1, 1: e2, 2: e3
+        if (on) todo &= todo - 1;
+        const int k0 = which == 0 ? k1 : which == 1 ? k2 : kq;
+        const int k9 = which == 0 ? kq : which == 1 ? k1 : kn;
         if (__ballot(on)) {
+          double sm = 0.0, sb = 0.0;
           const int rc = lsq_fit_lockstep(
               on, k9 - k0 + 1, [&](int i) { return (int)L.xn[k0 + i][lane]; },
               [&](int i) { return (double)L.ys[k0 + i][lane]; }, xtab, sm, sb);
-          if (on && rc < 0) status |= LT_ST_NUMERIC;
+          if (on) {
+            if (rc < 0) status |= LT_ST_NUMERIC;
+            const double x1 = (double)L.xn[k1][lane], xq = (double)L.xn[kq][lane];
+            if (which == 0) {
+              fr1 = (sm * x1) + sb;
+              flq = (sm * xq) + sb;
+            } else if (which == 1) {
+              fl1 = (sm * x1) + sb;
+            } else {
+              frq = (sm * xq) + sb;
+            }
+          }
         }
-      };
-      fit(act, k1, kq, m1, b1);
-      fit(has2, k2, k1, m2, b2);
-      fit(hasn, kq, kn, m3, b3);
-      // fitted values at vertices q-1 and q, as the walk computes them
-      auto vfit = [&](int k, bool two, double pm, double pb, double cm, double cb)
+      }
+      // fitted values at vertices q-1 and q, as the walk computes them (the closer eqn to the raw
+      // value, the left on a tie; a side pass A decided directly)
+      auto pick = [&](int k, bool left, bool right, double fl, double fr)
                       __attribute__((always_inline)) {
-        const double xv = (double)L.xn[k][lane];
-        const double fr = (cm * xv) + cb;
-        if (!two || (pm == cm && pb == cb)) return fr;
-        const double fl = (pm * xv) + pb;
+        if (left) return fl;
+        if (right) return fr;
         const double raw_v = (double)L.ys[k][lane];
         return __builtin_fabs(fl - raw_v) <= __builtin_fabs(fr - raw_v) ? fl : fr;
       };
-      const double f1 = vfit(k1, has2, m2, b2, m1, b1);
-      const double fq = hasn ? vfit(kq, true, m1, b1, m3, b3) : (m1 * (double)L.xn[kq][lane]) + b1;
+      const double f1 = has2 ? pick(k1, cl1, cr1, fl1, fr1) : fr1;
+      const double fq = hasn ? pick(kq, clq, crq, flq, frq) : flq;
       const int32_t on = y0 + (int32_t)L.xn[k1][lane];
       const int32_t du = (int32_t)L.xn[kq][lane] - (int32_t)L.xn[k1][lane];
 #pragma unroll

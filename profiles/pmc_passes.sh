@@ -8,6 +8,8 @@ OUT=$R/$1; shift
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 ARGS="$@"
+# the build the counters belong to, with this environment (summarize_pmc.py reads it)
+python3 -c "import sys; sys.path.insert(0, '$R'); from land_trendr_amd._abi import build_hash; print(build_hash())" > $OUT/_build.txt
 run() {
   name=$1; shift
   timeout -s KILL 240 rocprofv3 --pmc "$@" --output-format csv -d $OUT/$name -o run -- \

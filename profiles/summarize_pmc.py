@@ -42,10 +42,19 @@ def main(root, out, px=None, input_mode='bands'):
         row['launches'] = n
         res[name] = row
     res['_source'] = root
-    # the kernel build the counters belong to (bench.py compares it with its own)
-    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-    from land_trendr_amd._abi import build_hash
-    res['_build'] = build_hash()
+    # the kernel build the counters belong to (bench.py compares it with its own): the hash
+    # pmc_passes.sh recorded when it collected them (its environment included: a phase-cut or A/B
+    # run under LT_JIT_DEFINES etc. is another build), else computed now and marked so
+    stamp = os.path.join(root, '_build.txt')
+    if os.path.exists(stamp):
+        res['_build'] = open(stamp).read().strip()
+        res['_build_stamped'] = 'at collection (pmc_passes.sh)'
+    else:
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        from land_trendr_amd._abi import build_hash
+        res['_build'] = build_hash()
+        res['_build_stamped'] = 'at summary time (no _build.txt)'
+
     res['_pixels_per_launch'] = px
     res['_input'] = input_mode
     json.dump(res, open(out, 'w'), indent=1, sort_keys=True)
