@@ -48,9 +48,10 @@
 #define LT_CERT_RULES 4
 #endif
 // labels-only certified path, pass B: fit only the eqns whose side pass A left undecided, in
-// lockstep slots (1), or all three eqns of every candidate (0)
+// lockstep slots, or all three eqns of every candidate: a stage mask (bit 0 the analyze stage,
+// bit 1 the resolve stage: 3 slots in both, 0 in neither)
 #ifndef LT_PASSB_SLOTS
-#define LT_PASSB_SLOTS 1
+#define LT_PASSB_SLOTS 3
 #endif
 
 // Launch-uniform values a JIT kernel may be compiled for (lt_jit.h defines LT_SPEC_* for the
@@ -1627,7 +1628,7 @@ __device__ inline int analyze_fast(const DevScene& S_launch, const lt_params& P,
       // frq at vertex q), all the choice needs: where two eqns are identical their values are,
       // so the reference's "same eqn: the right one" shortcut gives the same value
       // (LT_PASSB_SLOTS=0, A/B runs: the three eqns always, each fitted whenever a lane has it)
-      const bool slots = LT_PASSB_SLOTS != 0 && !infdata;
+      const bool slots = ((LT_PASSB_SLOTS >> (EXACT ? 1 : 0)) & 1) && !infdata;
       const bool cl1 = slots && has2 && ((CL >> k1) & 1), cr1 = slots && has2 && ((CR >> k1) & 1);
       const bool clq = slots && hasn && ((CL >> kq) & 1), crq = slots && hasn && ((CR >> kq) & 1);
       unsigned todo = (act && !(cl1 && crq) ? 1u : 0u) | (has2 && !cr1 ? 2u : 0u) |

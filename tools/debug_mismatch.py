@@ -1,0 +1,125 @@
+"""Locate and isolate parity mismatches of a bench config's timed launch (debugging aid): runs
+bench.py's exact launch for --config, samples pixels against the oracle, lists mismatching pixels
+with the differing fields, then re-runs (a) those pixels alone and (b) their whole 64-pixel waves
+(original neighbours, original lane positions) through the same JIT path, to tell a per-pixel
+defect from a lockstep (wave-neighbour) one. Prints one JSON object."""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+from land_trendr_amd.distributed import Mosaic  # noqa: E402
+from land_trendr_amd.engine import get_engine, valid_bytes  # noqa: E402
+from land_trendr_amd.index_eqn import IndexProgram  # noqa: E402
+from land_trendr_amd.runner import MosaicRunner  # noqa: E402
+from land_trendr_amd.settings import compile_params  # noqa: E402
+from land_trendr_amd.synth import mosaic_inputs  # noqa: E402
+from oracle import oracle  # noqa: E402
+
+FIELDS = ['status', 'matched', 'class_val', 'onset_year', 'duration', 'magnitude']
+
+
+def same(a, b):
+    if a.dtype.kind == 'f':
+        return (a.view(np.int64) == b.view(np.int64)) | (np.isnan(a) & np.isnan(b))
+    return a == b
+
+
+def compare(want, got):
+    """{column: [differing fields]} (bench.parity_sample's comparison, per pixel)."""
+    bad = {}
+    m = want['matched'].astype(bool)
+    for f in FIELDS:
+        g = got[f]
+        e = want[f][:g.shape[0]] if g.ndim == 2 else want[f]
+        if f in ('class_val', 'onset_year', 'duration', 'magnitude'):
+            g, e = np.where(m[:g.shape[0]], g, 0), np.where(m[:g.shape[0]], e, 0)
+        s = same(e, g)
+        for c in np.where(~s.reshape(-1, s.shape[-1]).all(axis=0))[0]:
+            bad.setdefault(int(c), []).append(f)
+    return bad
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--config', default='c3')
+    ap.add_argument('--sample', type=int, default=200000)
+    ap.add_argument('--pixels', type=int, default=0)
+    a = ap.parse_args()
+    c = bench.CONFIGS[a.config]
+    P = a.pixels or c['pixels']
+    eng = get_engine(0)
+    dev = eng.device
+    m = Mosaic([P], P, 1, 0, 'by_scene')
+    items = mosaic_inputs(m, c['years'], c['k'][0], c['k'][1], c['mask'], c['seed'], dev,
+                          bench.TARGET)
+    params, _ = compile_params(c['line_cost'], c['rules'], c['mode'])
+    fn = eng.compile_index(IndexProgram('B1 - B2', band_dtype='int16'))
+    r = MosaicRunner(eng, m, params, items, FIELDS, fn)
+    r.step()
+    torch.cuda.synchronize()
+    first = {f: r.outs[0][f].clone() for f in FIELDS}
+    # determinism: the same launch again, every output plane compared bitwise with the first
+    r.step()
+    torch.cuda.synchronize()
+    diff = torch.zeros(P, dtype=torch.bool, device=dev)
+    for f in FIELDS:
+        a0, a1 = first[f], r.outs[0][f]
+        if a0.dtype.is_floating_point:
+            a0, a1 = a0.view(torch.int64), a1.view(torch.int64)
+        d = a0 != a1
+        diff |= d.reshape(-1, P).any(dim=0)
+    r.materialise_index(0)
+    torch.cuda.synchronize()
+    it = items[0]
+    rng = np.random.default_rng(5)
+    idx = np.sort(rng.choice(P, min(P, a.sample), replace=False))
+    cols = torch.from_numpy(idx).to(dev)
+    vals = it.values[:, cols].double().cpu().numpy()
+    vb = valid_bytes(it.valid[:, cols], it.scene.n_obs).cpu().numpy() if it.valid is not None else None
+    want = oracle.analyze_tile(it.scene, params, vals, vb, n_threads=min(os.cpu_count() or 1, 16))
+    got = {f: r.outs[0][f][..., cols].cpu().numpy() for f in FIELDS}
+    bad = compare(want, got)
+    bad_px = [int(idx[c]) for c in sorted(bad)]
+    res = {'config': a.config, 'jit_defines': os.environ.get('LT_JIT_DEFINES'),
+           'sampled': len(idx), 'mismatching_pixels': len(bad_px),
+           'step2_differs_from_step1_pixels': int(diff.sum()),
+           'mismatching_pixels_that_differ_between_steps': int(diff[cols].cpu().numpy()[sorted(bad)].sum()) if bad else 0,
+           'examples': [{'pixel': int(idx[c]), 'lane': int(idx[c]) % 64, 'fields': bad[c],
+                         'want': {f: (want[f][..., c].tolist()) for f in bad[c]},
+                         'got': {f: (got[f][..., c].tolist()) for f in bad[c]}}
+                        for c in sorted(bad)[:12]]}
+    if bad_px:
+        # (a) alone: the pixels side by side in one small tile; (b) their waves, same lanes
+        def rerun(pix):
+            pt = torch.tensor(pix, device=dev)
+            K = it.bands.shape[0]
+            inter = torch.empty((K, len(pix), 2), dtype=torch.int16, device=dev).permute(0, 2, 1)
+            inter.copy_(it.bands[:, :, pt])
+            valid = it.valid[:, pt].contiguous() if it.valid is not None else None  # bit planes
+            out = eng.analyze_tiles(it.scene, params, [(inter, valid)], FIELDS, index=fn)[0]
+            torch.cuda.synchronize()
+            g = {f: out[f].cpu().numpy() for f in FIELDS}
+            pos = [pix.index(p) for p in bad_px]
+            sel = torch.tensor(bad_px, device=dev)
+            v2 = it.values[:, sel].double().cpu().numpy()  # the index raster (materialised)
+            vb2 = valid_bytes(it.valid[:, sel], it.scene.n_obs).cpu().numpy() if it.valid is not None else None
+            w2 = oracle.analyze_tile(it.scene, params, v2, vb2)
+            g2 = {f: g[f][..., pos] for f in FIELDS}
+            return len(compare(w2, g2))
+        res['alone_mismatching'] = rerun(bad_px)
+        waves = sorted({p // 64 for p in bad_px})
+        wpix = [p for w in waves for p in range(w * 64, min(P, w * 64 + 64))]
+        res['in_their_waves_mismatching'] = rerun(wpix)
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == '__main__':
+    main()
