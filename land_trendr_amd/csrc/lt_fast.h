@@ -42,6 +42,12 @@
 #ifndef LT_AB_NO_FITS
 #define LT_AB_NO_FITS 0
 #endif
+// LT_AB_YEAR_SINK = 1: the year-major loop's plane stores all go to the pixel's year-0 row (the
+// same instructions and bytes leave the CUs, ~1/Y of them reach HBM), nontemporal; 2: the same
+// with ordinary stores (the rows then stay in L2)
+#ifndef LT_AB_YEAR_SINK
+#define LT_AB_YEAR_SINK 0
+#endif
 // labels-only launches of up to this many rules take the certified path (closed-form fits, the
 // emulated ones only around the rules' candidates); more rules keep one emulated fit per vertex
 #ifndef LT_CERT_RULES
@@ -202,6 +208,14 @@ __device__ inline int analyze_fast(const DevScene& S_launch, const lt_params& P,
   int status = LT_ST_OK;
   static_assert(LT_MAX_YEARS == 64, "one year-table word per lane");
   if (lane < Y) L.year[lane] = S.year[lane];
+#ifdef LT_DEBUG_LDS_POISON
+  // debugging (LT_JIT_DEFINES=LT_DEBUG_LDS_POISON=v): the lane's series slots filled with a junk
+  // pattern first, so a read of a slot this pixel did not write shows up as a changed result
+  for (int k = 0; k < MAXY; k++) {
+    L.ys[k][lane] = (VT)(LT_DEBUG_LDS_POISON + 37 * k);
+    L.xn[k][lane] = (uint8_t)(LT_DEBUG_LDS_POISON + 11 * k);
+  }
+#endif
   __syncthreads();  // one wave per workgroup: orders the table writes before any lane reads
 
   // ---- pick_winners (utils.py:491-521) over wave-uniform year slots ----
@@ -1390,12 +1404,17 @@ __device__ inline int analyze_fast(const DevScene& S_launch, const lt_params& P,
     // (16-byte stores of pixel pairs from the even lanes, the odd lane's value moved over by DPP:
     // c5 1083-1092 vs 1260 Mpx/s, profiles/r04_run19)
     auto store_row = [&](int yy, const Row& r) __attribute__((always_inline)) {
-      const int64_t o = (int64_t)yy * os + p;
+      const int64_t o = LT_AB_YEAR_SINK ? p : (int64_t)yy * os + p;
       // write-once planes: nontemporal stores (same-box c5 A/B: 1012 vs 896-925 Mpx/s). When
       // the year is present in every emitting lane (always, without a cloud mask) the values
       // are stored as they are: no NaN select pair per plane
       auto put = [&](double* plane, double v) __attribute__((always_inline)) {
-        if (plane && !LT_AB_NO_YEAR_STORES) __builtin_nontemporal_store(v, plane + o);
+        if (plane && !LT_AB_NO_YEAR_STORES) {
+          if (LT_AB_YEAR_SINK == 2)
+            plane[o] = v;
+          else
+            __builtin_nontemporal_store(v, plane + o);
+        }
       };
       if (r.uni) {
         put(out.val_fit, r.fv);

@@ -56,6 +56,13 @@ __device__ inline void analyze_body() {
   __shared__ WaveLds<MAXY, VT, false> L;
   const KernelArgs& K = args();
   const int lane = threadIdx.x;
+#ifdef LT_DEBUG_LDS_PAD
+  // debugging (LT_JIT_DEFINES=LT_DEBUG_LDS_PAD=bytes): extra LDS per workgroup, to run the
+  // analyze stage at a lower occupancy (fewer co-resident waves per CU) with the same code
+  __shared__ uint32_t lds_pad[LT_DEBUG_LDS_PAD / 4];
+  lds_pad[lane] = (uint32_t)lane;
+  asm volatile("" ::"v"(lds_pad[lane]));
+#endif
   const int64_t p = (int64_t)blockIdx.x * 64 + lane;
   const int64_t n_pix = K.in.n_pix;
   const bool live = p < n_pix;
