@@ -683,6 +683,9 @@ __host__ __device__ bool analyze_pixel(const DevScene& S, const lt_params& P, co
       n++;
     }
     // ---- segmented least squares DP (utils.py:618-631) ----
+#ifdef LT_HOST_DIAG
+    lt_host_diag_series(p, n, xs, ys);  // host diagnostics (tests/native): the DP's input series
+#endif
     uint8_t arg[MAXY];
     if constexpr (LAZY) {
       if (!dp_lazy<MAXY>(n, xs, ys, P.line_cost, arg)) return false;

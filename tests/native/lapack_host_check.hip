@@ -5,6 +5,18 @@
 // tests/native/build/liblt_hostcheck.so. Not part of the product (which has no CPU path).
 #include <string.h>
 
+// diagnostics hook of lt_pixel.h analyze_pixel: the compacted (non-spike) series the DP takes
+#define LT_HOST_DIAG 1
+static int g_diag_n = -1;
+static uint8_t g_diag_xs[64];
+static double g_diag_ys[64];
+static void lt_host_diag_series(long long, int n, const uint8_t* xs, const double* ys) {
+  g_diag_n = n;
+  for (int k = 0; k < n && k < 64; k++) {
+    g_diag_xs[k] = xs[k];
+    g_diag_ys[k] = ys[k];
+  }
+}
 #include "../../land_trendr_amd/csrc/lt_pixel.h"
 
 extern "C" int ltx_lstsq(int m, const double* x, const double* y, int want_solution,
@@ -149,4 +161,16 @@ extern "C" int ltx_rule_cands(int n, const int32_t* on, const int32_t* du, const
   return full.have == part.have && full.on == part.on && full.du == part.du &&
          same(full.mag, part.mag) && same(full.init, part.init) &&
          (n == 0 || st_cand == st_full);
+}
+
+// The DP's input series (after pick_winners, despike and dropna) of the last pixel
+// ltx_analyze_tile processed: returns n (-1: none reached the DP), fills xs / ys.
+extern "C" int ltx_last_series(uint8_t* xs, double* ys) {
+  for (int k = 0; k < g_diag_n; k++) {
+    xs[k] = g_diag_xs[k];
+    ys[k] = g_diag_ys[k];
+  }
+  const int n = g_diag_n;
+  g_diag_n = -1;
+  return n;
 }

@@ -125,6 +125,61 @@ def main():
                      'tiles_done_ms': [round(s0.elapsed_time(e), 3) for e in marks],
                      'transfer_done_after_ms': round(s0.elapsed_time(x1), 3),
                      'note': 'tiles 16.8 Mpx x 3; the copy waits for tile 0'}
+    # the same with the analyze / resolve launches on a CU-masked stream that leaves `free` CUs
+    # (the mask's last bits) to the transfer (hipExtStreamCreateWithCUMask): does a reserved
+    # slice let the blit (RCCL's P2P kernels likewise) progress beside analyze, and what does the
+    # analyze step lose?
+    import ctypes
+    hip = ctypes.CDLL('libamdhip64.so')
+    n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
+    for free in (8, 16):
+        words = (n_cu + 31) // 32
+        mask = (ctypes.c_uint32 * words)()
+        for cu in range(n_cu - free):
+            mask[cu // 32] |= 1 << (cu % 32)
+        hs = ctypes.c_void_p()
+        rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(hs), ctypes.c_uint32(words), mask)
+        if rc != 0:
+            res['cumask_error'] = rc
+            break
+        ms = torch.cuda.ExternalStream(hs.value, device=dev)
+        with torch.cuda.stream(ms):
+            r3.step()
+            torch.cuda.synchronize()
+            t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            t0.record()
+            for _ in range(3):
+                r3.step()
+            t1.record()
+            torch.cuda.synchronize()
+            masked_alone = t0.elapsed_time(t1) / 3
+            marks = []
+
+            def timed_events2(n):
+                evs = [torch.cuda.Event(enable_timing=True) for _ in range(n)]
+                for e in evs:
+                    e.record()
+                marks.extend(evs)
+                return evs
+            r3._done_events = timed_events2
+            s0, x1, t_end = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+            torch.cuda.synchronize()
+            s0.record()
+            r3.step()
+            side.wait_event(marks[0])
+            with torch.cuda.stream(side):
+                a.copy_(b, non_blocking=True)
+                x1.record()
+            t_end.record()
+            torch.cuda.synchronize()
+            del r3._done_events
+        res['cumask_free%d' % free] = {
+            'cus': n_cu, 'free_cus': free, 'step_alone_masked_ms': round(masked_alone, 3),
+            'step_ms': round(s0.elapsed_time(t_end), 3),
+            'tiles_done_ms': [round(s0.elapsed_time(e), 3) for e in marks],
+            'transfer_done_after_ms': round(s0.elapsed_time(x1), 3)}
+        torch.cuda.synchronize()
+        hip.hipStreamDestroy(hs)
     print(json.dumps(res), flush=True)
 
 
