@@ -48,6 +48,10 @@
 #ifndef LT_AB_YEAR_SINK
 #define LT_AB_YEAR_SINK 0
 #endif
+// the year-major loop's binary64 plane stores: 1 nontemporal (the default), 0 plain
+#ifndef LT_YEAR_NT
+#define LT_YEAR_NT 1
+#endif
 // labels-only launches of up to this many rules take the certified path (closed-form fits, the
 // emulated ones only around the rules' candidates); more rules keep one emulated fit per vertex
 #ifndef LT_CERT_RULES
@@ -1410,7 +1414,7 @@ __device__ inline int analyze_fast(const DevScene& S_launch, const lt_params& P,
       // are stored as they are: no NaN select pair per plane
       auto put = [&](double* plane, double v) __attribute__((always_inline)) {
         if (plane && !LT_AB_NO_YEAR_STORES) {
-          if (LT_AB_YEAR_SINK == 2)
+          if (LT_AB_YEAR_SINK == 2 || !LT_YEAR_NT)
             plane[o] = v;
           else
             __builtin_nontemporal_store(v, plane + o);

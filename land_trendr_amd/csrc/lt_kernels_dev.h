@@ -22,6 +22,19 @@ __device__ inline void defer_append(bool deferred, int64_t p, int lane, int64_t*
   if (deferred) list[base + __popcll(mask & ((1ull << lane) - 1))] = p;
 }
 
+// The pixel group of workgroup b (64 pixels each). LT_XCD_REMAP = 1: blocks are dealt round-robin
+// over the 8 XCDs (MI355X_MICROARCH.md § Workgroup dispatch, observed placement, speed only), so the
+// blocks sharing an XCD (equal b % 8) take one contiguous pixel range, in order: consecutive
+// groups' row pieces of a per-year plane then leave the same L2 close in time. 0: group b.
+#ifndef LT_XCD_REMAP
+#define LT_XCD_REMAP 0
+#endif
+__device__ inline int64_t xcd_block(unsigned b, unsigned G) {
+  if (!LT_XCD_REMAP) return (int64_t)b;
+  const unsigned x = b & 7u, i = b >> 3, q = G >> 3, r = G & 7u;  // bijective for any G
+  return (int64_t)x * q + (x < r ? x : r) + i;
+}
+
 // Every argument of the analyze / resolve kernels, passed as ONE by-value struct. The kernels read
 // its fields through the kernarg segment pointer at their uses (args()), so a field is loaded
 // where a stage needs it: a kernel that names its by-value parameters gets every one of them
@@ -63,7 +76,7 @@ __device__ inline void analyze_body() {
   lds_pad[lane] = (uint32_t)lane;
   asm volatile("" ::"v"(lds_pad[lane]));
 #endif
-  const int64_t p = (int64_t)blockIdx.x * 64 + lane;
+  const int64_t p = xcd_block(blockIdx.x, gridDim.x) * 64 + lane;
   const int64_t n_pix = K.in.n_pix;
   const bool live = p < n_pix;
   const int d = analyze_fast<MAXY, RMAX, false, VT>(*K.S, K.P, K.in, K.out, K.xtab, K.yflags,

@@ -52,6 +52,7 @@ def main():
     ap.add_argument('--config', default='c3')
     ap.add_argument('--sample', type=int, default=200000)
     ap.add_argument('--pixels', type=int, default=0)
+    ap.add_argument('--no-rerun', action='store_true', help='skip the isolation reruns')
     a = ap.parse_args()
     c = bench.CONFIGS[a.config]
     P = a.pixels or c['pixels']
@@ -65,10 +66,12 @@ def main():
     r = MosaicRunner(eng, m, params, items, FIELDS, fn)
     r.step()
     torch.cuda.synchronize()
+    print('step 1 done', file=sys.stderr, flush=True)
     first = {f: r.outs[0][f].clone() for f in FIELDS}
     # determinism: the same launch again, every output plane compared bitwise with the first
     r.step()
     torch.cuda.synchronize()
+    print('step 2 done', file=sys.stderr, flush=True)
     diff = torch.zeros(P, dtype=torch.bool, device=dev)
     for f in FIELDS:
         a0, a1 = first[f], r.outs[0][f]
@@ -76,6 +79,8 @@ def main():
             a0, a1 = a0.view(torch.int64), a1.view(torch.int64)
         d = a0 != a1
         diff |= d.reshape(-1, P).any(dim=0)
+    print(json.dumps({'step2_differs_from_step1_pixels': int(diff.sum())}), file=sys.stderr,
+          flush=True)
     r.materialise_index(0)
     torch.cuda.synchronize()
     it = items[0]
@@ -96,7 +101,7 @@ def main():
                          'want': {f: (want[f][..., c].tolist()) for f in bad[c]},
                          'got': {f: (got[f][..., c].tolist()) for f in bad[c]}}
                         for c in sorted(bad)[:12]]}
-    if bad_px:
+    if bad_px and not a.no_rerun:
         # (a) alone: the pixels side by side in one small tile; (b) their waves, same lanes
         def rerun(pix):
             pt = torch.tensor(pix, device=dev)
