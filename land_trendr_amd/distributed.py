@@ -144,7 +144,7 @@ class LabelExchange:
         self._send_stream = (torch.cuda.Stream(self.device)
                              if not self.is_writer and self.device.type == 'cuda' and
                              not self._staged and mosaic.world > 1 else None)
-        self._works = []
+        self._works = []   # (round, work) in posting order
 
     def slab(self, tile):
         return self._slabs[tile.t]
@@ -185,14 +185,15 @@ class LabelExchange:
         if ops:
             if self._recv_stream is not None:
                 with torch.cuda.stream(self._recv_stream):
-                    self._works += d.batch_isend_irecv(ops)
+                    works = d.batch_isend_irecv(ops)
             elif after is not None and self._send_stream is not None:
                 # RCCL's stream waits for the send stream, which waits for this tile alone
                 with torch.cuda.stream(self._send_stream):
                     self._send_stream.wait_event(after)
-                    self._works += d.batch_isend_irecv(ops)
+                    works = d.batch_isend_irecv(ops)
             else:
-                self._works += d.batch_isend_irecv(ops)
+                works = d.batch_isend_irecv(ops)
+            self._works += [(k, w) for w in works]
 
     def post_all(self):
         for k in range(self.m.rounds):
@@ -200,10 +201,30 @@ class LabelExchange:
 
     def wait(self):
         while self._works:
-            self._works.pop(0).wait()
+            self._works.pop(0)[1].wait()
         for buf, dst in self._staged_in:
             dst.copy_(buf)
         self._staged_in, self._staged_out = [], []
+
+    @property
+    def can_overlap(self):
+        """Whether a round's ops may stay in flight past the step that posted them (RCCL: ops
+        are stream-ordered; gloo's staged host copies need wait() in the step)."""
+        return self.m.world > 1 and not self._staged
+
+    def wait_round(self, k):
+        """The current stream waits for the ops of round k posted so far (a previous step's send
+        of slab k, before this step's kernels write it again); other rounds stay in flight. The
+        writer's kernels write only its own slabs, which it never sends: nothing to wait for."""
+        if self.is_writer:
+            return
+        keep = []
+        for kk, w in self._works:
+            if kk == k:
+                w.wait()
+            else:
+                keep.append((kk, w))
+        self._works = keep
 
     def checksums(self, tiles):
         """Position-weighted byte sums, one per (tile, field), of the slabs of `tiles` as this

@@ -168,19 +168,24 @@ class MosaicRunner:
         if g:
             yield g
 
-    def step(self, timed=False, after_tile=None, stage_in=None, slab_free=None):
+    def step(self, timed=False, after_tile=None, stage_in=None, slab_free=None, overlap=False):
         """Queue one pass over this rank's tiles and complete the label exchange.
         after_tile(k): called once tile k's kernels are queued (e.g. to stream its trendline).
         stage_in: an object whose fetch(k) -> (bands, event) supplies tile k's band planes from
         elsewhere (an H2D copy the load kernel waits for) and whose consumed(k, event) learns
         when the load kernel has read them. slab_free(j): with a ring, the event (or None)
-        after which tile j's ring buffer is free again; tile j + ring waits for it."""
+        after which tile j's ring buffer is free again; tile j + ring waits for it.
+        overlap: the label exchange of this step stays in flight past its return (RCCL): the
+        next step's kernels for tile k wait only for this step's send of tile k's slab, so the
+        last tiles' transfers overlap the next step's first tiles (a stream of scenes); call
+        finish() after the last step. Ignored where the exchange cannot overlap (gloo)."""
         eng = self.eng
         if not self.cuda:
             timed = False
         if self.ring and self.cuda and slab_free is None:
             raise ValueError('a ring of output buffers needs slab_free')
         self._slab_free = slab_free
+        self._overlap = bool(overlap) and self.exchange.can_overlap
         if self.fused:
             return self._step_fused(after_tile, stage_in)
         main = torch.cuda.current_stream(eng.device) if self.cuda else None
@@ -216,6 +221,7 @@ class MosaicRunner:
             scene = self.items[g[0]].scene
             n = [self.items[k].tile.n for k in g]
             self._wait_ring(g[0])
+            self._wait_sends(g)
             done = self._done_events(len(g))
             eng.analyze_tiles(
                 scene, self.params, [(self.items[k].values, self.items[k].valid) for k in g],
@@ -234,7 +240,8 @@ class MosaicRunner:
         for k in range(len(self.items), self.m.rounds):
             self.exchange.post(k)
         self._join(pending)
-        self.exchange.wait()
+        if not self._overlap:
+            self.exchange.wait()
 
     def _step_fused(self, after_tile, stage_in):
         """step() with the fused load stage: each tile's analyze kernel reads its band planes.
@@ -256,6 +263,7 @@ class MosaicRunner:
                     ready = [ev_in]
                 tiles.append((bands, self.items[k].valid))
             self._wait_ring(g[0])
+            self._wait_sends(g)
             done = self._done_events(len(g))
             eng.analyze_tiles(
                 scene, self.params, tiles, self.fields,
@@ -273,6 +281,19 @@ class MosaicRunner:
         for k in range(len(self.items), self.m.rounds):
             self.exchange.post(k)
         self._join(pending)
+        if not self._overlap:
+            self.exchange.wait()
+
+    def _wait_sends(self, g):
+        """With overlap: before tiles g are written again, the stream waits for the previous
+        step's sends of their slabs (a sender; the writer's receives are ordered on RCCL's
+        stream, and its own slabs are not sent)."""
+        if getattr(self, '_overlap', False):
+            for k in g:
+                self.exchange.wait_round(k)
+
+    def finish(self):
+        """Complete every exchange still in flight (after steps run with overlap=True)."""
         self.exchange.wait()
 
     def _wait_ring(self, k):

@@ -29,7 +29,7 @@ def _free_port():
     return port
 
 
-def _run(world, rank, scene_px, tile, assign, seed0, dist=None, dst=0):
+def _run(world, rank, scene_px, tile, assign, seed0, dist=None, dst=0, steps=1, overlap=False):
     from land_trendr_amd.engine import IndexFn
     from land_trendr_amd.index_eqn import IndexProgram
     from land_trendr_amd.runner import MosaicRunner
@@ -40,16 +40,21 @@ def _run(world, rank, scene_px, tile, assign, seed0, dist=None, dst=0):
     params, _ = compile_params(10, RULES)
     fn = IndexFn(None, IndexProgram('B1 - B2', band_dtype='int16'))
     r = MosaicRunner(OracleEngine(), m, params, items, FIELDS, fn, dist, dst=dst)
-    r.step()
+    for _ in range(steps):
+        r.step(overlap=overlap)
+    r.finish()
     return r
 
 
-def _worker(rank, world, port, scene_px, tile, assign, result_path, dst=0):
+def _worker(rank, world, port, scene_px, tile, assign, result_path, dst=0, steps=1,
+            overlap=False):
     import torch.distributed as dist
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(port)
     dist.init_process_group('gloo', rank=rank, world_size=world)
-    r = _run(world, rank, scene_px, tile, assign, 7, dist, dst)
+    r = _run(world, rank, scene_px, tile, assign, 7, dist, dst, steps, overlap)
+    if overlap:  # the steps ran pipelined: some sends stayed in flight past their step
+        assert r._overlap
     # bench.py's exchange check: the owners' per-tile checksums, all-reduced, equal the writer's
     tot = r.exchange.checksums(r.m.mine)
     dist.all_reduce(tot)
@@ -122,6 +127,26 @@ def test_multi_rank_exchange_matches_single_process(tmp_path, world, px, tile, a
     path = str(tmp_path / 'r.npz')
     mp.spawn(_worker, args=(world, _free_port(), px, tile, assign, path, dst), nprocs=world,
              join=True)
+    got = np.load(path)
+    want = _want(px, 7)
+    for f in ltd.LABEL_GATHER_FIELDS:
+        assert _same(want[f][:2], got[f]), f
+
+
+@pytest.mark.parametrize('world,px,tile,assign,dst', [
+    (2, [600, 600], 256, 'by_scene', 0),     # the c2 shape
+    (2, [700, 300], 256, 'round_robin', 0),  # the c4 shape
+    (3, [300, 200, 900], 256, 'by_scene', 2),  # unequal scenes, writer rank 2
+])
+@pytest.mark.timeout(180)
+def test_pipelined_exchange_over_steps_matches_single_process(tmp_path, world, px, tile, assign,
+                                                              dst):
+    """bench.py's timed loop at N > 1: three steps with overlap=True (each step's sends stay in
+    flight into the next; a sender's kernels for tile k first wait for the previous send of
+    tile k's slab), then finish(): the writer holds exactly the single-process result."""
+    path = str(tmp_path / 'r.npz')
+    mp.spawn(_worker, args=(world, _free_port(), px, tile, assign, path, dst, 3, True),
+             nprocs=world, join=True)
     got = np.load(path)
     want = _want(px, 7)
     for f in ltd.LABEL_GATHER_FIELDS:
