@@ -52,6 +52,26 @@
 #ifndef LT_YEAR_NT
 #define LT_YEAR_NT 1
 #endif
+// cache policy of the per-year binary64 row stores (year-major planes and val_raw): 0 the
+// compiler's nontemporal store (nt: the line stays in the XCD's L2), 1 sc1 (write-through, the
+// line dropped from L2: MI355X_MICROARCH.md, store flavours), 2 sc0 sc1, 3 nt sc1
+#ifndef LT_YEAR_STORE_MODE
+#define LT_YEAR_STORE_MODE 0
+#endif
+
+namespace lt {
+__device__ inline void year_row_store(double v, double* a) {
+#if LT_YEAR_STORE_MODE == 1
+  asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(a), "v"(v) : "memory");
+#elif LT_YEAR_STORE_MODE == 2
+  asm volatile("global_store_dwordx2 %0, %1, off sc0 sc1" ::"v"(a), "v"(v) : "memory");
+#elif LT_YEAR_STORE_MODE == 3
+  asm volatile("global_store_dwordx2 %0, %1, off sc1 nt" ::"v"(a), "v"(v) : "memory");
+#else
+  __builtin_nontemporal_store(v, a);
+#endif
+}
+}  // namespace lt
 // labels-only launches of up to this many rules take the certified path (closed-form fits, the
 // emulated ones only around the rules' candidates); more rules keep one emulated fit per vertex
 #ifndef LT_CERT_RULES
@@ -466,7 +486,7 @@ __device__ inline int analyze_fast(const DevScene& S_launch, const lt_params& P,
         }
         pres |= 1ull << y;
         T++;
-        if (out.val_raw && LT_AB_NO_YEAR_STORES < 2) __builtin_nontemporal_store(v, out.val_raw + q);
+        if (out.val_raw && LT_AB_NO_YEAR_STORES < 2) year_row_store(v, out.val_raw + q);
       } else if (out.val_raw && LT_AB_NO_YEAR_STORES < 2) {  // the other per-year planes: the year-major output loop
         __builtin_nontemporal_store(nan, out.val_raw + q);
       }
@@ -1417,7 +1437,7 @@ __device__ inline int analyze_fast(const DevScene& S_launch, const lt_params& P,
           if (LT_AB_YEAR_SINK == 2 || !LT_YEAR_NT)
             plane[o] = v;
           else
-            __builtin_nontemporal_store(v, plane + o);
+            year_row_store(v, plane + o);
         }
       };
       if (r.uni) {
