@@ -1,6 +1,7 @@
 #!/bin/bash
 # r05 run 19: VALU / SALU instructions per wave by phase (PMC of the JIT analyze kernel cut after
-# each phase, LT_JIT_STOP_AFTER=k, one 16.8 Mpx c2 / c3 launch each; timing-only builds)
+# each phase, LT_JIT_STOP_AFTER=k, one 16.8 Mpx c2 / c3 launch each; timing-only builds), and c5
+# without the winner pick's winner-row stores (timing-only: what a separate fill launch would save)
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/${1:-gpurun_out/r05_run19}
@@ -25,4 +26,10 @@ print(sys.argv[1].split('/')[-1], 'launches', len(disp), 'waves/launch %.0f' % w
                if k.startswith('SQ_INSTS') and w))
 PY
   done
+done
+cd $R
+for v in base nowinner; do
+  if [ $v = nowinner ]; then export LT_JIT_DEFINES=LT_AB_NO_WINNER_STORE=1; else unset LT_JIT_DEFINES; fi
+  timeout -k 10 170 python bench.py --config c5 --steps 5 --no-cpu-baseline --e2e-steps 0 --tiled-steps 0 --parity-sample 0 > $O/c5_$v.json 2> $O/c5_$v.err
+  python -c "import json;d=json.load(open('$O/c5_$v.json'));print('c5 $v',round(d['value'],1),d['ms_per_step'],d['roofline']['kernel_ms'])"
 done
