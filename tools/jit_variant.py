@@ -7,7 +7,9 @@ generator's scheduling of waits (debugging aid, not the product):
 
 writes <out>/lt_src_<FNV-1a of the source>.co; a run with LT_JIT_OVERRIDE_DIR=<out> (and the same
 LT_JIT_DEFINES) loads it instead of compiling that source. --defines are passed the way
-LT_JIT_DEFINES passes them (part of the generated source, so of its hash).
+LT_JIT_DEFINES passes them (part of the generated source, so of its hash). --hdr-root builds it
+from modified copies of the kernel headers (A/B of a source change without rebuilding the
+library: the generated source, and so the override's name, does not include the headers).
 """
 import argparse
 import ctypes
@@ -20,12 +22,12 @@ sys.path.insert(0, os.path.join(ROOT, 'tools'))
 sys.path.insert(0, ROOT)
 
 
-def compile_rtc(src, opts, arch='gfx950'):
+def compile_rtc(src, opts, arch='gfx950', hdr_root=ROOT):
     import __graft_entry__ as ge
     rtc = ctypes.CDLL('/opt/rocm/lib/libhiprtc.so')
     names, texts = [], []
     for rel in ge.JIT_HEADERS:
-        with open(os.path.join(ROOT, rel)) as fh:
+        with open(os.path.join(hdr_root, rel)) as fh:
             texts.append(fh.read().replace('#include "../../include/lt_abi.h"',
                                            '#include "lt_abi.h"').encode())
         names.append(os.path.basename(rel).encode())
@@ -60,11 +62,15 @@ def main():
     ap.add_argument('--out', required=True)
     ap.add_argument('--define', action='append', default=[])
     ap.add_argument('--opt', action='append', default=[])
+    ap.add_argument('--hdr-root', default=ROOT,
+                    help='a tree holding modified copies of the kernel headers (same layout): the '
+                         'override is built from them, the library and its build hash stay as '
+                         'they are')
     a = ap.parse_args()
     if a.define:
         os.environ['LT_JIT_DEFINES'] = ','.join(a.define)
     src = jit_isa.jit_source(a.config)
-    code = compile_rtc(src, a.opt)
+    code = compile_rtc(src, a.opt, hdr_root=a.hdr_root)
     os.makedirs(a.out, exist_ok=True)
     name = os.path.join(a.out, 'lt_src_%016x.co' % jit_asm.fnv1a(src.encode()))
     with open(name, 'wb') as fh:
