@@ -53,19 +53,20 @@
 enum Kind { ADD_U32, CNDMASK, CMP, FMA_F32, FMA_F32K, ADD_F64, FMA_F64, MUL_F64, RCP_F64, LSHL_B64,
             MIX_C2, MOV_B32, CNDMASK_VCC, CNDMASK_VCC_VALU, CMP_CNDMASK_VCC, CNDMASK_E64_VCC,
             CNDMASK_E64_SMOV, CNDMASK_E64_VCMP, MOV_B64, CMP_E32, NOP_MIX, CMP_CND2_VCC,
-            CMP_CND4_VCC, CMP_GAP_CND_VCC, CMP64_CND2, NKIND };
+            CMP_CND4_VCC, CMP_GAP_CND_VCC, CMP64_CND2, MAD_U64, MAD_U24, MUL_LO, NKIND };
 static const char* kKindName[NKIND] = {"add_u32", "cndmask_b32", "cmp_gt_u32", "fma_f32",
                                        "fma_f32_k", "add_f64", "fma_f64", "mul_f64", "rcp_f64",
                                        "lshlrev_b64", "mix_c2", "mov_b32", "cndmask_b32_vcc",
                                        "cndmask_vcc_valu", "cmp_cndmask_vcc", "cndmask_e64_vcc",
                                        "cndmask_e64_smov", "cndmask_e64_vcmp", "mov_b64",
                                        "cmp_e32", "nop_mix", "cmp_cnd2_vcc", "cmp_cnd4_vcc",
-                                       "cmp_gap_cnd_vcc", "cmp64_cnd2"};
+                                       "cmp_gap_cnd_vcc", "cmp64_cnd2", "mad_u64_u32", "mad_u32_u24",
+                                       "mul_lo_u32"};
 // VALU / SALU instructions per loop iteration of each kind (the asm blocks below)
 static const int kValuPerIter[NKIND] = {64, 64, 64, 64, 64, 64, 64, 64, 32, 64, 103, 64, 64,
-                                        65, 64, 64, 64, 65, 64, 64, 64, 48, 80, 80, 48};
+                                        65, 64, 64, 64, 65, 64, 64, 64, 48, 80, 80, 48, 64, 64, 64};
 static const int kSaluPerIter[NKIND] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 50, 0, 1,
-                                        0, 0, 1, 1, 0, 0, 0, 8, 0, 0, 0, 0};
+                                        0, 0, 1, 1, 0, 0, 0, 8, 0, 0, 0, 0, 0, 0, 0};
 
 #define R8(s) s s s s s s s s
 
@@ -176,6 +177,28 @@ __global__ void __launch_bounds__(64) valu_kernel(unsigned* out, unsigned long l
                    : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7),
                      "+s"(m0)
                    : "v"(inc), "v"(t));
+    } else if constexpr (K == MAD_U64) {  // the 32 x 32 + 64 multiply-add the compiler uses for
+      // an int32 a*a + s whose operands it cannot prove 24-bit (the DP's Sxx += x*x)
+      asm volatile(R8("v_mad_u64_u32 %0, %8, %9, %9, %0\n v_mad_u64_u32 %1, %8, %9, %9, %1\n"
+                      "v_mad_u64_u32 %2, %8, %9, %9, %2\n v_mad_u64_u32 %3, %8, %9, %9, %3\n"
+                      "v_mad_u64_u32 %4, %8, %9, %9, %4\n v_mad_u64_u32 %5, %8, %9, %9, %5\n"
+                      "v_mad_u64_u32 %6, %8, %9, %9, %6\n v_mad_u64_u32 %7, %8, %9, %9, %7\n")
+                   : "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3), "+v"(q4), "+v"(q5), "+v"(q6), "+v"(q7),
+                     "=s"(m1)
+                   : "v"(inc));
+    } else if constexpr (K == MAD_U24) {  // the full-rate 24-bit multiply-add
+      asm volatile(R8("v_mad_u32_u24 %0, %8, %8, %0\n v_mad_u32_u24 %1, %8, %8, %1\n"
+                      "v_mad_u32_u24 %2, %8, %8, %2\n v_mad_u32_u24 %3, %8, %8, %3\n"
+                      "v_mad_u32_u24 %4, %8, %8, %4\n v_mad_u32_u24 %5, %8, %8, %5\n"
+                      "v_mad_u32_u24 %6, %8, %8, %6\n v_mad_u32_u24 %7, %8, %8, %7\n")
+                   : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)
+                   : "v"(inc));
+    } else if constexpr (K == MUL_LO) {  // v_mul_lo_u32 (32 x 32, low half)
+      asm volatile(R8("v_mul_lo_u32 %0, %0, %8\n v_mul_lo_u32 %1, %1, %8\n v_mul_lo_u32 %2, %2, %8\n"
+                      "v_mul_lo_u32 %3, %3, %8\n v_mul_lo_u32 %4, %4, %8\n v_mul_lo_u32 %5, %5, %8\n"
+                      "v_mul_lo_u32 %6, %6, %8\n v_mul_lo_u32 %7, %7, %8\n")
+                   : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)
+                   : "v"(inc));
     } else if constexpr (K == MOV_B64) {  // 64-bit moves (a rotation of eight register pairs)
       asm volatile(R8("v_mov_b64 %0, %1\n v_mov_b64 %1, %2\n v_mov_b64 %2, %3\n v_mov_b64 %3, %4\n"
                       "v_mov_b64 %4, %5\n v_mov_b64 %5, %6\n v_mov_b64 %6, %7\n v_mov_b64 %7, %0\n")
@@ -358,6 +381,9 @@ static KFn kernel_of(int k) {
     case CMP_CND4_VCC: return valu_kernel<CMP_CND4_VCC>;
     case CMP_GAP_CND_VCC: return valu_kernel<CMP_GAP_CND_VCC>;
     case CMP64_CND2: return valu_kernel<CMP64_CND2>;
+    case MAD_U64: return valu_kernel<MAD_U64>;
+    case MAD_U24: return valu_kernel<MAD_U24>;
+    case MUL_LO: return valu_kernel<MUL_LO>;
     default: return valu_kernel<MIX_C2>;
   }
 }
