@@ -1009,6 +1009,9 @@ __device__ inline int analyze_fast(const DevScene& S_launch, const lt_params& P,
       // gv/gi/gt: the best zero-residual start on an inexact OPTa of the group's base (its
       // interval enters the trackers at the end of the column)
       double Ve = inf, Hi = inf, L1 = inf, L2 = inf, v1 = inf, gv = inf;
+      // U = min(Hi, Ve, gh), kept as each of them changes (each only decreases): the column's
+      // current upper bound without recomputing it per start
+      double U = inf;
       int ie = 0, i1 = 0, iL = -1, n1 = -1, gi = -1, gt = 0;
       uint64_t cand = 0;  // resolve stage: the >= 3-point starts an exact decision prices
       // (the bounds Hi, L1, L2 are only compared: v_min_f64 instead of a select pair; the values
@@ -1020,6 +1023,7 @@ __device__ inline int analyze_fast(const DevScene& S_launch, const lt_params& P,
           n1 = nt;
         }
         Hi = __builtin_fmin(hi, Hi);
+        U = __builtin_fmin(U, hi);
         const bool bl = lo <= L1;
         L2 = bl ? L1 : __builtin_fmin(lo, L2);
         L1 = __builtin_fmin(lo, L1);
@@ -1035,6 +1039,7 @@ __device__ inline int analyze_fast(const DevScene& S_launch, const lt_params& P,
             Ve = v;
             ie = i;
           }
+          U = __builtin_fmin(U, v);
           return;
         }
         const double w = __builtin_fma(0x1p-50, __builtin_fabs(v), Emax);
@@ -1044,6 +1049,7 @@ __device__ inline int analyze_fast(const DevScene& S_launch, const lt_params& P,
           gt = tg;
           gv = v;
           gh = v + w;
+          U = __builtin_fmin(U, gh);
         } else if (ord == 0) {
           track(i, v, v + w, v - w, tg < 0 ? -1 : tg + 1);
         }  // ord < 0: strictly above the group's best, never the first minimum
@@ -1076,6 +1082,7 @@ __device__ inline int analyze_fast(const DevScene& S_launch, const lt_params& P,
           }
         }
       }
+      U = __builtin_fmin(__builtin_fmin(Hi, Ve), gh);
       // prefix bound for the early exit below: every segment ending at j has Syy <= SyyAll
       wx0 = L.xn[j][lane];
       wy0 = (double)L.ys[j][lane];
@@ -1146,9 +1153,7 @@ __device__ inline int analyze_fast(const DevScene& S_launch, const lt_params& P,
       // an upper bound on the column minimum so far (it only decreases as starts are added). A
       // start whose lower end lies above it can change no decision: it is neither the smallest
       // upper end nor among the lower ends at or below the final minimum bound H
-      auto upper = [&]() __attribute__((always_inline)) {
-        return __builtin_fmin(__builtin_fmin(Hi, Ve), gh);
-      };
+      auto upper = [&]() __attribute__((always_inline)) { return U; };
       // start i (>= 3 points, its point already in the sums): priced, offered to the trackers when
       // its lower end reaches the column's current upper bound (else it can change no decision),
       // its early-exit bound returned
