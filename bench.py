@@ -374,7 +374,11 @@ def main():
     dev = torch.device('cuda', local)
     mosaic_cfg = 'scenes' in cfg
     if mosaic_cfg:  # one mosaic for the whole job, tiles round-robin over the ranks
-        tile = args.tile or ((P + 7) // 8 + 63) // 64 * 64
+        # four tiles per rank (at N = 8 the 32 tiles of P / 8 the round-robin was built for; at
+        # N = 1 one launch per scene, as c2: 32 launches of 6.1 Mpx ran 2615 Mpx/s, each paying
+        # a launch drain), no tile larger than a scene
+        total = P * cfg['scenes']
+        tile = args.tile or min(P, ((total + 4 * world - 1) // (4 * world) + 63) // 64 * 64)
         mosaic = Mosaic([P] * cfg['scenes'], tile, world, rank, 'round_robin')
     else:  # one scene per rank (weak scaling)
         # one launch per scene on one GPU for the labels-only configs (fewer launch drains and
