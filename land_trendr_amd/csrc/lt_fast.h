@@ -563,32 +563,30 @@ __device__ inline int analyze_fast(const DevScene& S_launch, const lt_params& P,
         z[u] = (int)L.ys[tz][lane];
         xo[u] = (int)L.xn[tx][lane];
       }
+      // branch-free per point: every lane takes every step (a lane past its last point, or
+      // without one, only rewrites the slot past its compacted series and keeps n), so the wave
+      // runs no exec-mask juggling per point; the last point is never a spike (mid)
 #pragma unroll
       for (int u = 0; u < 8; u++) {
         const int t = t0 + u;
         if (t >= Tmax) break;  // wave-uniform
-        if (!(ok && t < T)) continue;
+        const bool inr = ok && t < T;  // the lane has point t
         const int cur = yv;
-        bool is_spike = false;
-        if (t + 1 < T) {  // the last point is never a spike
-          const int zv = z[u];
-          const int d1 = yv - xv, d2 = zv - yv;
-          // not monotone (x <= y <= z or x >= y >= z fails: the steps have strictly opposite
-          // signs) with both |steps| >= K: as K >= 1, one step >= K and the other <= -K
-          const bool big = (d1 >= K && d2 <= nK) || (d1 <= nK && d2 >= K);
-          is_spike = big && yv != last_good;
-          if (!is_spike) last_good = yv;
-          xv = yv;
-          yv = zv;
-        }
-        if (is_spike) {
-          spike |= 1ull << t;
-          continue;
-        }
-        // (slot n = t before the first spike: the same values rewritten, no branch)
+        const int zv = z[u];
+        const int d1 = yv - xv, d2 = zv - yv;
+        // not monotone (x <= y <= z or x >= y >= z fails: the steps have strictly opposite
+        // signs) with both |steps| >= K: as K >= 1, one step >= K and the other <= -K
+        const bool big = (d1 >= K && d2 <= nK) || (d1 <= nK && d2 >= K);
+        const bool is_spike = inr && t + 1 < T && big && yv != last_good;
+        last_good = is_spike ? last_good : yv;  // (a lane past its points never reads it)
+        xv = yv;
+        yv = zv;
+        spike |= is_spike ? (1ull << t) : 0ull;
+        // slot n gets point t; n moves on for a kept point (slot n = t before the first spike:
+        // the same values rewritten)
         L.ys[n][lane] = (VT)cur;
         L.xn[n][lane] = (uint8_t)xo[u];
-        n++;
+        n += (inr && !is_spike) ? 1 : 0;
       }
     }
   } else if (Tmax >= 2) {
