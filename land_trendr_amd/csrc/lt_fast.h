@@ -248,6 +248,13 @@ __device__ inline int analyze_fast(const DevScene& S_launch, const lt_params& P,
   // int16 series: the values are integers of int16 range, so despike's standard deviation is
   // compared through the exact sums S = sum v, Q = sum v^2 (see the despike below)
   constexpr bool kIntSeries = std::is_same<VT, int16_t>::value;
+  // a JIT kernel specialised for labels-only launches takes the branch-free store loop below (in
+  // the per-year-output instances the same loop measured 1 % slower, profiles/r05_run29)
+#if defined(LT_SPEC_YEAR_OUT) && LT_SPEC_YEAR_OUT == 0
+  constexpr bool kFlatPick = true;
+#else
+  constexpr bool kFlatPick = false;
+#endif
   double Ssum = 0.0, Qsum = 0.0;
   bool f32_bad = false;
   bool intdata = true;  // every value an integer of int16 range (lt_pixel.h sse_exact_zero)
@@ -459,7 +466,28 @@ __device__ inline int analyze_fast(const DevScene& S_launch, const lt_params& P,
 #pragma unroll
     for (int u = 0; u < WB; u++) {
       const int y = yb + u;
-      if (y >= Y || !live) continue;
+      if (y >= Y) break;  // wave-uniform
+      if constexpr (kIntSeries && kFlatPick) {
+        // labels-only int16 series, branch-free: every lane takes the step; a lane without the
+        // year (or dead) writes slot T (its next point overwrites it; past its series it is never
+        // read) and keeps T and the sums (c2 +1.4 %, c3 +1.1 %, profiles/r05_run29)
+        if (!out.winner && !out.val_raw) {  // launch-uniform
+          const bool pr = live && best[u] >= 0;
+          if ((S.feb29_mask >> y) & 1) status |= pr ? LT_ST_FEB29 : 0;
+          const double v = val[u];
+          const int ty = S.year[y];
+          y0 = (pr && T == 0) ? ty : y0;
+          L.ys[T][lane] = (VT)v;
+          L.xn[T][lane] = (uint8_t)(ty - y0);
+          const double vp = pr ? v : 0.0;
+          Ssum += vp;
+          Qsum = __builtin_fma(vp, vp, Qsum);
+          pres |= pr ? 1ull << y : 0ull;
+          T += pr ? 1 : 0;
+          continue;
+        }
+      }
+      if (!live) continue;
       const int64_t q = (int64_t)y * os + p;
       if (out.winner && LT_AB_NO_YEAR_STORES < 2)
         __builtin_nontemporal_store((int16_t)best[u], out.winner + q);
