@@ -1,8 +1,10 @@
 #!/bin/bash
 # r05 run 30: the JIT modules compiled with other AMDGPU machine-scheduler settings (override code
 # objects of the product's c2 / c3 sources, tools/jit_variant.py --opt): max-ilp, max-memory-clause,
-# the AMDGPU register-pressure trackers, no unclustered high-RP reschedule; A/B against the
-# product build, twice, parity samples on
+# the AMDGPU register-pressure trackers, no unclustered high-RP reschedule; and V15 (the lazy DP's
+# per-start ballots taken of single compares, masked by ballots taken once per column / per DP:
+# no VGPR 0/1 round trip per test), V16 (V15 + the LDS start loop's counter in an SGPR); A/B
+# against the product build, twice, parity samples on
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/${1:-gpurun_out/r05_run30}
@@ -20,5 +22,10 @@ for i in 1 2; do
     for V in maxilp memclause trk nounc; do
       b ${C}_${V}_$i s_$V "--config $C"
     done
+    b ${C}_v15_$i v15 "--config $C"
+    b ${C}_v16_$i v16 "--config $C"
   done
+  b c5_base_$i "" "--config c5"
+  b c5_v15_$i v15 "--config c5"
+  b c5_v16_$i v16 "--config c5"
 done
