@@ -943,6 +943,7 @@ __device__ inline int analyze_fast(const DevScene& S_launch, const lt_params& P,
     // zero-residual starts of >= 3 points (lt_pixel.h kZero): integer series of int16 range only
     const bool zok = c > 0.0;
     const bool zlane = zok && intdata;
+    const uint64_t zmask = __ballot(zlane);
     uint64_t amb = 0;
     // resolve stage: the exact decision of column j for the lanes xr (see column below). One
     // lockstep loop of emulated residuals: per lane first the links k (OPTa[k] = fl(fl(e(a, k-1) +
@@ -1028,6 +1029,7 @@ __device__ inline int analyze_fast(const DevScene& S_launch, const lt_params& P,
                       double& opt_jm2, double& opt_jm3, int& tg_j, int& tg_jm1, int& tg_jm2,
                       int& tg_jm3) __attribute__((always_inline)) {
       const bool col = j < n;
+      const uint64_t colmask = __ballot(col);
       double Sy = 0.0, Sxy = 0.0, Syy = 0.0;
       int Sx = 0, Sxx = 0;
       // interval candidates: smallest upper end (Hi: start i1, value v1, tag n1 of OPTa[j+1] if it
@@ -1148,7 +1150,7 @@ __device__ inline int analyze_fast(const DevScene& S_launch, const lt_params& P,
         hi = v + w;
         lo = v - w;
         bnd = dp_start_bound_slack(e, o, wopt, c, slack);
-        return zlane && e <= ws;
+        return e <= ws;  // (zlane applied by the caller: see zmask)
       };
       // exactly collinear with a residual that rounds away (lt_pixel.h kZero, sse_exact_zero), on
       // sums of integer data (exact binary64 integers)
@@ -1164,12 +1166,10 @@ __device__ inline int analyze_fast(const DevScene& S_launch, const lt_params& P,
       // a start of >= 3 points: a zero-residual start (v recomputed as the reference's
       // fl(c + OPTa[i])) or an interval candidate that starts a new base if it wins
       auto offer = [&](int i, double o, int tg, double v, double hi, double lo, bool zr) __attribute__((always_inline)) {
-        if (__ballot(zr)) {
-          if (zr) {
-            zero_start(i, c + o, tg);
-            hi = inf;  // kept out of the trackers (an infinite upper end never decides)
-            lo = inf;
-          }
+        if (zr) {
+          zero_start(i, c + o, tg);
+          hi = inf;  // kept out of the trackers (an infinite upper end never decides)
+          lo = inf;
         }
         track(i, v, hi, lo, -1);
       };
@@ -1191,10 +1191,17 @@ __device__ inline int analyze_fast(const DevScene& S_launch, const lt_params& P,
         if constexpr (EXACT) {
           if (!(lo > upper())) cand |= 1ull << i;
         }
+        // (each ballot of a single compare, masked by a ballot taken once: a ballot of a compound
+        // condition is materialised in a VGPR as 0 / 1 and compared again, two VALU per test)
         if (__ballot(lo <= upper())) {
-          bool zr = false;
-          if (__ballot(nz)) zr = nz && zero_test(j - i + 1, Sx, Sxx, Sy, Sxy, Syy);
-          offer(i, o, tg, v, hi, lo, zr);
+          if (__ballot(nz) & zmask) {  // rare: exactly collinear candidates
+            const bool zr = zlane && nz && zero_test(j - i + 1, Sx, Sxx, Sy, Sxy, Syy);
+            if (__ballot(zr)) {
+              offer(i, o, tg, v, hi, lo, zr);
+              return bnd;
+            }
+          }
+          track(i, v, hi, lo, -1);
         }
         return bnd;
       };
@@ -1203,7 +1210,7 @@ __device__ inline int analyze_fast(const DevScene& S_launch, const lt_params& P,
       // bound, so tracking it changes no decision. The starts go one at a time, each with its own
       // exit test (pricing two per exit test: 2115 vs 2231 Mpx/s on c2, profiles/r02_ab_dp)
       auto leave = [&](double bnd) __attribute__((always_inline)) {
-        return prune && !__ballot(col && !(bnd > upper()));
+        return prune && (__ballot(!(bnd > upper())) & colmask) == 0;
       };
       bool more = j >= 2;  // wave-uniform
       if (more) {  // starts j-2 and j-3 from the register window
@@ -1215,11 +1222,15 @@ __device__ inline int analyze_fast(const DevScene& S_launch, const lt_params& P,
         }
         more = more && j >= 3;
       }
-      for (int ii = j - 4; more && ii >= 0; ii--) {  // the rest from LDS / private memory
-        const int i = __builtin_amdgcn_readfirstlane(ii);  // wave-uniform start
-        add_xy(L.xn[i][lane], (double)L.ys[i][lane]);
-        // tags are kept in the window only: a start from private memory is exact or not
-        if (leave(one_start(i, OPTa[i], ((exact >> i) & 1) ? 0 : -1))) break;
+      if (more) {  // the rest from LDS / private memory
+        // the start index in an SGPR through the loop (a VGPR counter cost a VALU decrement and
+        // a readfirstlane per start)
+        for (int i = __builtin_amdgcn_readfirstlane(j - 4); i >= 0;
+             i = __builtin_amdgcn_readfirstlane(i - 1)) {
+          add_xy(L.xn[i][lane], (double)L.ys[i][lane]);
+          // tags are kept in the window only: a start from private memory is exact or not
+          if (leave(one_start(i, OPTa[i], ((exact >> i) & 1) ? 0 : -1))) break;
+        }
       }
       // the group's best enters the trackers (an empty group: gv = inf, no effect)
       {
