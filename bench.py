@@ -329,7 +329,8 @@ def main():
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-overlap', action='store_true',
-                    help='N > 1: complete each step\'s label exchange before the next step')
+                    help='complete each step (its last resolve / expand stages, and at N > 1 '
+                         'its label exchange) before the next step starts')
     ap.add_argument('--e2e-steps', type=int, default=1,
                     help='end-to-end steps (H2D bands, D2H outputs) after the timed ones; 0: none')
     ap.add_argument('--group', type=int, default=0,
@@ -419,9 +420,10 @@ def main():
     eng.stage_ms()  # reset
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    # at N > 1 each step's label exchange stays in flight into the next step (runner.step
-    # overlap: tile k's kernels wait only for the previous step's send of tile k), as for a
-    # stream of scenes; every transfer is complete before the clock stops (finish)
+    # the steps are pipelined as for a stream of scenes (runner.step overlap): a step's last
+    # resolve runs beside the next step's first analyze, and at N > 1 its label exchange stays in
+    # flight into the next step (tile k's kernels wait only for the previous step's send of tile
+    # k); every tile's stages and transfers are complete before the clock stops (finish)
     for _ in range(args.steps):
         runner.step(timed=True, overlap=not args.no_overlap)
     runner.finish()
@@ -612,6 +614,7 @@ def main():
                    'gather': bool(gather),
                    'exchange_pipelined': bool(gather and runner.exchange.can_overlap
                                               and not args.no_overlap),
+                   'steps_pipelined': not args.no_overlap,
                    'input': 'int16 bands B1, B2 + index_eqn "%s"' % args.index_eqn +
                             (' (fused into the analyze kernel%s)'
                              % (': JIT kernels, lt_jit.h' if runner.jit is not None else '')

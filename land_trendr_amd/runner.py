@@ -122,9 +122,10 @@ class MosaicRunner:
         self.index_events = []  # (start, stop) pairs of the timed steps' load kernels
 
     def _done_events(self, n):
-        """Per-tile completion events for a call whose tiles' labels are exchanged (created by a
-        first record, so the library's record on its own stream is the one waited for), or None."""
-        if not (self.gathering and self.cuda):
+        """Per-tile completion events for a call whose tiles' labels are exchanged, or whose last
+        stages run on past the step (pipelined steps), created by a first record so the library's
+        record on its own stream is the one waited for; or None."""
+        if not ((self.gathering or getattr(self, '_pipe', False)) and self.cuda):
             return None
         evs = [torch.cuda.Event() for _ in range(n)]
         for e in evs:
@@ -175,10 +176,15 @@ class MosaicRunner:
         elsewhere (an H2D copy the load kernel waits for) and whose consumed(k, event) learns
         when the load kernel has read them. slab_free(j): with a ring, the event (or None)
         after which tile j's ring buffer is free again; tile j + ring waits for it.
-        overlap: the label exchange of this step stays in flight past its return (RCCL): the
-        next step's kernels for tile k wait only for this step's send of tile k's slab, so the
-        last tiles' transfers overlap the next step's first tiles (a stream of scenes); call
-        finish() after the last step. Ignored where the exchange cannot overlap (gloo)."""
+        overlap: the step's work stays in flight past its return, as for a stream of scenes; call
+        finish() after the last step. The label exchange (RCCL; not gloo, whose staged copies
+        complete in the step): the next step's kernels for tile k wait only for this step's send
+        of tile k's slab, so the last tiles' transfers overlap the next step's first tiles. The
+        tiles' last stages (resolve, trendline expand; on a GPU, without a ring or stage_in): the
+        current stream does not wait for them at the step's end, so the last tile's resolve runs
+        beside the next step's first analyze as consecutive tiles of one call do (the library
+        reuses a deferred-list set only after its resolve; a step's analyze writes no output of
+        a pixel it defers, so the overlapping stages write disjoint pixels)."""
         eng = self.eng
         if not self.cuda:
             timed = False
@@ -186,6 +192,7 @@ class MosaicRunner:
             raise ValueError('a ring of output buffers needs slab_free')
         self._slab_free = slab_free
         self._overlap = bool(overlap) and self.exchange.can_overlap
+        self._pipe = bool(overlap) and self.cuda and not self.ring and stage_in is None
         if self.fused:
             return self._step_fused(after_tile, stage_in)
         main = torch.cuda.current_stream(eng.device) if self.cuda else None
@@ -239,9 +246,7 @@ class MosaicRunner:
         # nothing left to post
         for k in range(len(self.items), self.m.rounds):
             self.exchange.post(k)
-        self._join(pending)
-        if not self._overlap:
-            self.exchange.wait()
+        self._end_step(pending)
 
     def _step_fused(self, after_tile, stage_in):
         """step() with the fused load stage: each tile's analyze kernel reads its band planes.
@@ -280,9 +285,7 @@ class MosaicRunner:
             pending += done or []
         for k in range(len(self.items), self.m.rounds):
             self.exchange.post(k)
-        self._join(pending)
-        if not self._overlap:
-            self.exchange.wait()
+        self._end_step(pending)
 
     def _wait_sends(self, g):
         """With overlap: before tiles g are written again, the stream waits for the previous
@@ -292,8 +295,20 @@ class MosaicRunner:
             for k in g:
                 self.exchange.wait_round(k)
 
+    def _end_step(self, pending):
+        """The step's outputs complete in stream order (joined), or, pipelined, left to finish()."""
+        if getattr(self, '_pipe', False):
+            self._pending = getattr(self, '_pending', []) + pending
+        else:
+            self._join(pending)
+        if not self._overlap:
+            self.exchange.wait()
+
     def finish(self):
-        """Complete every exchange still in flight (after steps run with overlap=True)."""
+        """Complete every tile and exchange still in flight (after steps run with overlap=True):
+        the current stream waits for every tile's last stage."""
+        self._join(getattr(self, '_pending', []))
+        self._pending = []
         self.exchange.wait()
 
     def _wait_ring(self, k):

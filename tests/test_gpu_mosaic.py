@@ -174,3 +174,42 @@ def test_stage_in_and_trendline_stream_match_resident_path():
                 assert row == y and key == k
                 want = ref[k][f][y, :n].cpu().contiguous().view(torch.uint8)
                 assert torch.equal(host, want), (f, k, y)
+
+
+@pytest.mark.parametrize('cfg', ['c3', 'c5'])
+def test_pipelined_steps_match_joined_step(cfg):
+    """bench.py's timed loop on one GPU: runner.step(overlap=True) leaves each tile's last stages
+    (resolve; with trendline planes the expand kernel) in flight past the step, so a step's last
+    resolve runs beside the next step's first analyze. After finish() every output equals what a
+    joined step writes (c3: cloud-mask bit planes and 3 rules; c5: all 15 fields)."""
+    fields = ['status', 'matched', 'class_val', 'onset_year', 'duration', 'magnitude']
+    if cfg == 'c5':
+        fields += bench.TRENDLINE_FIELDS
+    c = bench.CONFIGS[cfg]
+    m = Mosaic([3 * (1 << 20) + 4321], 1 << 20, 1, 0, 'by_scene')
+    eng = get_engine(0)
+    items = mosaic_inputs(m, c['years'], c['k'][0], c['k'][1], c['mask'], c['seed'], eng.device,
+                          bench.TARGET)
+    params, _ = compile_params(c['line_cost'], c['rules'], c['mode'])
+    fn = eng.compile_index(IndexProgram('B1 - B2', band_dtype='int16'))
+    runner = MosaicRunner(eng, m, params, items, fields, fn)
+    runner.step()
+    torch.cuda.synchronize()
+    assert eng.last_deferred() > 0  # the resolve stage has work in every step
+    ref = [{f: t.clone() for f, t in o.items()} for o in runner.outs]
+    for o in runner.outs:
+        for t in o.values():
+            t.fill_(7)
+    for _ in range(3):
+        runner.step(overlap=True)
+    assert len(runner._pending) == 3 * len(items)  # no step joined its tiles' last stages
+    runner.finish()
+    torch.cuda.synchronize()
+    for k, (o, r) in enumerate(zip(runner.outs, ref)):
+        n = items[k].tile.n
+        for f in fields:
+            a, b = o[f][..., :n], r[f][..., :n]
+            same = (a == b) | (torch.isnan(a) & torch.isnan(b)) if a.is_floating_point() else a == b
+            assert bool(same.all()), (cfg, k, f)
+    del runner
+    torch.cuda.empty_cache()
