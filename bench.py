@@ -493,6 +493,20 @@ def main():
     K0 = it0.scene.n_obs
     index_bytes = K0 * it0.tile.n * 6  # two int16 band planes read, one int16 plane written
 
+    # the dominant kernel with no previous step's resolve beside it: in the pipelined timed steps
+    # each analyze launch shares the CUs with the previous step's resolve for part of its time
+    # (its HIP-event time includes that); two joined steps, their HIP-event stage times
+    kern_ms_joined = None
+    if not args.no_overlap:
+        eng.set_timing(True)
+        eng.stage_ms()  # reset
+        for _ in range(2):
+            runner.step()
+        torch.cuda.synchronize()
+        st2 = eng.stage_ms()
+        eng.set_timing(False)
+        kern_ms_joined = st2['analyze'] / max(1, st2['launches'])
+
     e2e = None
     if args.e2e_steps > 0:
         if dist is not None:
@@ -548,7 +562,8 @@ def main():
         torch.cuda.synchronize()
         t3 = time.perf_counter()
         for _ in range(args.tiled_steps):
-            r3.step()
+            r3.step(overlap=not args.no_overlap)
+        r3.finish()
         torch.cuda.synchronize()
         dt3 = time.perf_counter() - t3
         tiled = {'tile_pixels': m3.tile, 'tiles': len(m3.tiles), 'steps': args.tiled_steps,
@@ -633,6 +648,10 @@ def main():
                      'frac': r(achieved / peak_g if achieved else None),
                      # against the same mix at the kernel's own occupancy (4 waves per SIMD,
                      # 128 VGPRs): how close the kernel is to what its occupancy allows
+                     # the same kernel in joined steps (no resolve of a previous step beside it)
+                     'kernel_ms_joined': r(kern_ms_joined, 3),
+                     'frac_joined': r(valu_px * px_per_launch / (kern_ms_joined * 1e-3) / 1e9 /
+                                      peak_g if valu_px and kern_ms_joined else None),
                      'frac_at_kernel_occupancy': r(
                          achieved / peak_cyc['mix_c2_at_4_waves_g_per_s']
                          if achieved and peak_cyc else None),
