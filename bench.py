@@ -496,16 +496,35 @@ def main():
     # the dominant kernel with no previous step's resolve beside it: in the pipelined timed steps
     # each analyze launch shares the CUs with the previous step's resolve for part of its time
     # (its HIP-event time includes that); two joined steps, their HIP-event stage times
+    #  and the whole-step rate of joined steps, beside the pipelined headline: a
+    # pipelined step is safe for inputs that change between steps (runner.step, tile_done), but
+    # the job runner's per-tile ring (job.py) runs joined steps
     kern_ms_joined = None
+    joined = None
     if not args.no_overlap:
         eng.set_timing(True)
         eng.stage_ms()  # reset
-        for _ in range(2):
+        n_joined = 2
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        tj = time.perf_counter()
+        for _ in range(n_joined):
             runner.step()
         torch.cuda.synchronize()
+        tj = time.perf_counter() - tj
         st2 = eng.stage_ms()
         eng.set_timing(False)
         kern_ms_joined = st2['analyze'] / max(1, st2['launches'])
+        tjt = torch.tensor([tj], dtype=torch.float64, device=dev)
+        if dist is not None:
+            dist.all_reduce(tjt, op=dist.ReduceOp.MAX)
+        tj = float(tjt.item())
+        joined = {'value': round(mosaic.n_pix * n_joined / tj / 1e6, 3), 'unit': 'Mpixels/s',
+                  'steps': n_joined, 'ms_per_step': round(tj / n_joined * 1e3, 3),
+                  'note': 'each step completes (every resolve, every transfer) before the next '
+                          'starts: the job runner\'s mode; `value` pipelines consecutive steps '
+                          '(runner.step overlap, safe for changing inputs)'}
 
     e2e = None
     if args.e2e_steps > 0:
@@ -712,6 +731,7 @@ def main():
         'resolve_stage': {'ms_per_launch': round(resolve_ms, 3),
                           'deferred_pixels_last_tile': n_deferred_last,
                           'last_tile_pixels': items[-1].tile.n},
+        'joined_steps': joined,
         'end_to_end': e2e,
         'n_gt_1_tiling': None if tiled is None else dict(
             tiled, ratio_to_value=round(tiled['value'] / value, 4)),

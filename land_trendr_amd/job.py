@@ -214,10 +214,15 @@ class LocalJob:
             copied[k] = tls.push({f: runner.outs[k][f] for f in tl_fields}, t.n, t)
 
         # tile k-1's rows are queued behind tile k's kernels, so the copies overlap them
-        runner.step(after_tile=(lambda k: push(k - 1) if k > 0 else None) if cuda else None,
-                    slab_free=copied.get if cuda else None)
+        try:
+            runner.step(after_tile=(lambda k: push(k - 1) if k > 0 else None) if cuda else None,
+                        slab_free=copied.get if cuda else None)
+        finally:
+            # the engine is cached per device (get_engine): a failed step must not leave later
+            # jobs of this process in async-JIT mode
+            if jit_async:
+                eng.set_jit_mode(False)
         if jit_async:
-            eng.set_jit_mode(False)
             self.jit_stats = eng.jit_stats()
         if cuda:
             if items:

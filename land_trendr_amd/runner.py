@@ -120,6 +120,14 @@ class MosaicRunner:
                             if self.cuda and has_bands and load_stream and not self.fused
                             else None)
         self.index_events = []  # (start, stop) pairs of the timed steps' load kernels
+        # pipelined steps (step(overlap=True)): the tiles' completion events not yet joined, the
+        # last completion event of every (bank, tile)'s output planes, and the output banks
+        self._pending = []
+        self._prev_done = {}
+        self._inflight = False  # a step left tiles or transfers in flight (finish() joins them)
+        self._ex_fields = tuple(ex)
+        self._banks = [self.outs]
+        self._bank = 0
 
     def _done_events(self, n):
         """Per-tile completion events for a call whose tiles' labels are exchanged, or whose last
@@ -180,19 +188,35 @@ class MosaicRunner:
         finish() after the last step. The label exchange (RCCL; not gloo, whose staged copies
         complete in the step): the next step's kernels for tile k wait only for this step's send
         of tile k's slab, so the last tiles' transfers overlap the next step's first tiles. The
-        tiles' last stages (resolve, trendline expand; on a GPU, without a ring or stage_in): the
-        current stream does not wait for them at the step's end, so the last tile's resolve runs
-        beside the next step's first analyze as consecutive tiles of one call do (the library
-        reuses a deferred-list set only after its resolve; a step's analyze writes no output of
-        a pixel it defers, so the overlapping stages write disjoint pixels)."""
+        tiles' last stages (resolve, trendline expand; on a GPU with the fused load stage, without
+        a ring or stage_in): the current stream does not wait for them at the step's end, so the
+        last tile's resolve runs beside the next step's first analyze as consecutive tiles of one
+        call do. Safe for inputs that change between steps:
+          * tile k's analyze kernel waits (lt_analyze_tiles_ev `ready`) for the completion event
+            of the last step that wrote the same output planes, so no resolve of an earlier step
+            writes them while a later step's analyze does (a pixel deferred in one step but not
+            in the next would otherwise keep the earlier step's value);
+          * a runner of ONE tile alternates between two banks of its output planes (self.outs
+            names the bank the last step wrote): its next step writes the other bank, so its
+            analyze still runs beside the previous step's resolve;
+          * a caller that rewrites tile k's INPUT planes (bands, mask) between pipelined steps
+            first makes its stream wait for tile_done(k): the previous step's resolve reads them.
+        overlap=False after pipelined steps completes them first (finish())."""
         eng = self.eng
         if not self.cuda:
             timed = False
         if self.ring and self.cuda and slab_free is None:
             raise ValueError('a ring of output buffers needs slab_free')
+        if not overlap and self._inflight:
+            self.finish()  # ADVICE r05: a joined step after pipelined ones joins them first
         self._slab_free = slab_free
         self._overlap = bool(overlap) and self.exchange.can_overlap
-        self._pipe = bool(overlap) and self.cuda and not self.ring and stage_in is None
+        # (the unfused load path writes it.values on the load stream while the previous step's
+        # resolve may still read them: pipelined steps need the fused load stage, ADVICE r05)
+        self._pipe = (bool(overlap) and self.cuda and not self.ring and stage_in is None and
+                      self.fused)
+        if self._pipe and len(self.items) == 1:
+            self._flip_bank()
         if self.fused:
             return self._step_fused(after_tile, stage_in)
         main = torch.cuda.current_stream(eng.device) if self.cuda else None
@@ -270,10 +294,17 @@ class MosaicRunner:
             self._wait_ring(g[0])
             self._wait_sends(g)
             done = self._done_events(len(g))
+            if self._pipe:  # tile k waits for the last step that wrote its planes (see step)
+                ready = [self._prev_done.get((self._bank, k)) for k in g]
+                if not any(e is not None for e in ready):
+                    ready = None
             eng.analyze_tiles(
                 scene, self.params, tiles, self.fields,
                 outs=[{f: x[..., :nk] for f, x in self.outs[k].items()} for k, nk in zip(g, n)],
                 ready=ready, lin=self.lin, index=self.jit, **self._ev_kw(done))
+            if done is not None:
+                for j, k in enumerate(g):
+                    self._prev_done[(self._bank, k)] = done[j]
             if stage_in is not None:
                 ev = torch.cuda.Event()
                 ev.record(main)
@@ -287,6 +318,27 @@ class MosaicRunner:
             self.exchange.post(k)
         self._end_step(pending)
 
+    def _flip_bank(self):
+        """A one-tile runner's pipelined step writes the other bank of its output planes (the
+        exchanged label slabs are shared: they are waited for through the tile's done event)."""
+        if len(self._banks) == 1:
+            o = self._banks[0][0]
+            self._banks.append([{f: (x if f in self._ex_fields else torch.empty_like(x))
+                                 for f, x in o.items()}])
+        self._bank ^= 1
+        self.outs = self._banks[self._bank]
+        if any(f in self._ex_fields for f in self.outs[0]):
+            # the shared slabs: the other bank's last writer must be complete as well
+            other = self._prev_done.get((self._bank ^ 1, 0))
+            if other is not None:
+                self._prev_done[(self._bank, 0)] = other
+
+    def tile_done(self, k):
+        """The event after which the last step's outputs of tile k are complete and its input
+        planes are no longer read (pipelined steps; None: the current stream's order suffices).
+        A caller that rewrites tile k's inputs between pipelined steps waits for it first."""
+        return self._prev_done.get((self._bank, k)) if self._pending else None
+
     def _wait_sends(self, g):
         """With overlap: before tiles g are written again, the stream waits for the previous
         step's sends of their slabs (a sender; the writer's receives are ordered on RCCL's
@@ -298,17 +350,22 @@ class MosaicRunner:
     def _end_step(self, pending):
         """The step's outputs complete in stream order (joined), or, pipelined, left to finish()."""
         if getattr(self, '_pipe', False):
-            self._pending = getattr(self, '_pending', []) + pending
+            self._pending = self._pending + pending
+            self._inflight = True
         else:
             self._join(pending)
         if not self._overlap:
             self.exchange.wait()
+        else:
+            self._inflight = True
 
     def finish(self):
         """Complete every tile and exchange still in flight (after steps run with overlap=True):
         the current stream waits for every tile's last stage."""
-        self._join(getattr(self, '_pending', []))
+        self._join(self._pending)
         self._pending = []
+        self._prev_done = {}
+        self._inflight = False
         self.exchange.wait()
 
     def _wait_ring(self, k):

@@ -213,3 +213,58 @@ def test_pipelined_steps_match_joined_step(cfg):
             assert bool(same.all()), (cfg, k, f)
     del runner
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize('tiles', [1, 3])
+def test_pipelined_steps_with_changing_inputs_match_joined_steps(tiles):
+    """a pipelined step (overlap=True) whose inputs differ from the previous step's.
+    The caller rewrites every tile's bands between two pipelined steps (after waiting for the
+    tile's tile_done event, the contract of runner.step); the outputs after finish() must equal
+    a joined step over the new inputs in every plane — also for pixels the first step deferred
+    and the second did not, whose stale resolve result would otherwise survive. tiles=1: the
+    one-launch geometry bench.py times (two output banks); tiles=3: per-tile waits."""
+    fields = ['status', 'matched', 'class_val', 'onset_year', 'duration', 'magnitude']
+    c = bench.CONFIGS['c3']
+    P = 3 * (1 << 20) + 4321
+    m = Mosaic([P], P if tiles == 1 else 1 << 20, 1, 0, 'by_scene')
+    eng = get_engine(0)
+    params, _ = compile_params(c['line_cost'], c['rules'], c['mode'])
+    fn = eng.compile_index(IndexProgram('B1 - B2', band_dtype='int16'))
+
+    def inputs():
+        return mosaic_inputs(m, c['years'], c['k'][0], c['k'][1], c['mask'], c['seed'],
+                             eng.device, bench.TARGET)
+
+    g = torch.Generator(device='cpu').manual_seed(99)
+    deltas = [torch.randint(-300, 301, (it.bands.shape[0], it.bands.shape[2]), generator=g,
+                            dtype=torch.int16).to(eng.device) for it in inputs()]
+    a_items = inputs()
+    a = MosaicRunner(eng, m, params, a_items, fields, fn)
+    a.step()
+    torch.cuda.synchronize()
+    a.step(overlap=True)  # scene X, left in flight
+    cur = torch.cuda.current_stream(eng.device)
+    for k, it in enumerate(a_items):  # scene Y: the caller's rewrite, after tile_done(k)
+        ev = a.tile_done(k)
+        assert ev is not None
+        cur.wait_event(ev)
+        it.bands[:, 0, :] += deltas[k]
+    a.step(overlap=True)
+    assert len(a._pending) > 0
+    a.finish()
+    torch.cuda.synchronize()
+    b_items = inputs()
+    for k, it in enumerate(b_items):
+        it.bands[:, 0, :] += deltas[k]
+    b = MosaicRunner(eng, m, params, b_items, fields, fn)
+    b.step()
+    torch.cuda.synchronize()
+    assert eng.last_deferred() > 0  # pixels go through the resolve stage in these steps
+    for k in range(len(a_items)):
+        n = a_items[k].tile.n
+        for f in fields:
+            x, y = a.outs[k][f][..., :n], b.outs[k][f][..., :n]
+            same = (x == y) | (torch.isnan(x) & torch.isnan(y)) if x.is_floating_point() else x == y
+            assert bool(same.all()), (tiles, k, f, int((~same).sum()))
+    del a, b, a_items, b_items
+    torch.cuda.empty_cache()

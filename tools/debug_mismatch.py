@@ -79,8 +79,14 @@ def main():
             a0, a1 = a0.view(torch.int64), a1.view(torch.int64)
         d = a0 != a1
         diff |= d.reshape(-1, P).any(dim=0)
-    print(json.dumps({'step2_differs_from_step1_pixels': int(diff.sum())}), file=sys.stderr,
-          flush=True)
+    # where in the launch the run-to-run differences sit: 64 equal bins over the pixel range
+    # (blocks are dispatched in order, so a bin is a span of dispatch time), and the first ones
+    dix = torch.nonzero(diff).flatten().cpu().numpy()
+    where = {'step2_differs_from_step1_pixels': int(diff.sum()),
+             'diff_hist64': np.histogram(dix, bins=64, range=(0, P))[0].tolist(),
+             'diff_first': dix[:40].tolist(),
+             'diff_lane_hist': np.bincount(dix % 64, minlength=64).tolist()}
+    print(json.dumps(where), file=sys.stderr, flush=True)
     r.materialise_index(0)
     torch.cuda.synchronize()
     it = items[0]
@@ -96,6 +102,8 @@ def main():
     res = {'config': a.config, 'jit_defines': os.environ.get('LT_JIT_DEFINES'),
            'sampled': len(idx), 'mismatching_pixels': len(bad_px),
            'step2_differs_from_step1_pixels': int(diff.sum()),
+           'diff_hist64': where['diff_hist64'], 'diff_first': where['diff_first'],
+           'diff_lane_hist': where['diff_lane_hist'],
            'mismatching_pixels_that_differ_between_steps': int(diff[cols].cpu().numpy()[sorted(bad)].sum()) if bad else 0,
            'examples': [{'pixel': int(idx[c]), 'lane': int(idx[c]) % 64, 'fields': bad[c],
                          'want': {f: (want[f][..., c].tolist()) for f in bad[c]},
