@@ -94,6 +94,8 @@ CONFIGS = {
 }
 TRENDLINE_FIELDS = ['winner', 'val_raw', 'val_fit', 'fit_m', 'fit_b', 'right_m', 'right_b',
                     'spike', 'vertex']
+# the label planes a rank copies to its host in the end-to-end 'own' mode (what the gather sends)
+LABEL_D2H_FIELDS = ['status', 'matched', 'class_val', 'onset_year', 'duration', 'magnitude']
 
 
 def f_ref(n):
@@ -279,31 +281,41 @@ class _PinnedBands:
         self.free[k % 2] = ev
 
 
-def end_to_end(runner, cfg, steps):
+def end_to_end(runner, cfg, steps, labels='gather'):
     """Steps of the same pipeline with the data movement a job has: each tile's int16 bands H2D
-    from pinned host memory before its load kernel (_PinnedBands), the writer's label rasters
-    D2H after the exchange, and for trendline configs every per-year plane of every tile D2H
-    through TrendlineStream (tile k-1's planes queued behind tile k's kernels).
-    Returns (seconds, H2D bytes, D2H bytes)."""
+    from pinned host memory before its load kernel (_PinnedBands), the label rasters D2H, and for
+    trendline configs every per-year plane of every tile D2H through TrendlineStream (tile k-1's
+    planes queued behind tile k's kernels). labels: 'gather' — the writer's label rasters D2H
+    after the exchange (every rank's labels cross the writer's one PCIe link); 'own' — the runner
+    exchanges nothing and each rank copies its own tiles' label planes to its host, tile k-1's
+    behind tile k's kernels (the writer's link would otherwise carry N scenes'
+    labels per step). Returns (seconds, H2D bytes, D2H bytes)."""
     dev = runner.eng.device
     stage = _PinnedBands(runner.items, dev)
-    d2h = TrendlineStream(runner.m.tile * 8, dev, depth=8) if cfg['trendline'] else None
+    tl = list(TRENDLINE_FIELDS) if cfg['trendline'] else []
+    own = [f for f in LABEL_D2H_FIELDS if f in runner.fields] if labels == 'own' else []
+    W = runner.m.tile
+    d2h = TrendlineStream(W * 8, dev, depth=8) if (tl or own) else None
     ex = runner.exchange
     lab_host = ({f: torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
-                 for f, t in ex.full.items()} if ex.is_writer else {})
+                 for f, t in ex.full.items()} if labels == 'gather' and ex.is_writer and ex.full
+                else {})
     items = runner.items
     bytes_d2h = 0
 
+    def planes(k):
+        return {f: runner.outs[k][f] for f in tl + own}
+
     def after(k):
         if d2h is not None and k > 0:
-            d2h.push({f: runner.outs[k - 1][f] for f in TRENDLINE_FIELDS}, items[k - 1].tile.n)
+            d2h.push(planes(k - 1), items[k - 1].tile.n)
 
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
         runner.step(after_tile=after, stage_in=stage)
-        if d2h is not None:
-            d2h.push({f: runner.outs[-1][f] for f in TRENDLINE_FIELDS}, items[-1].tile.n)
+        if d2h is not None and items:
+            d2h.push(planes(len(items) - 1), items[-1].tile.n)
         for f, t in lab_host.items():  # the writer's label rasters, for its GeoTIFF writer
             t.copy_(ex.full[f], non_blocking=True)
             bytes_d2h += t.numel() * t.element_size()
@@ -346,6 +358,13 @@ def main():
     ap.add_argument('--tiled-steps', type=int, default=3,
                     help='N = 1, labels-only configs: steps of the N > 1 tiling (16.8 Mpx tiles) '
                          'timed after the main ones (0: skip)')
+    ap.add_argument('--strong', action='store_true',
+                    help='strong scaling of ONE scene (the north_star shape: one 7000 x 7000 '
+                         'scene over N GPUs): its pixel tiles dealt round-robin to the ranks, '
+                         'labels sent to rank 0 (default: one scene per GPU, weak scaling)')
+    ap.add_argument('--e2e-labels', choices=('auto', 'gather', 'own'), default='auto',
+                    help='end-to-end steps: the writer copies the gathered label rasters to its '
+                         'host (gather), or every rank copies its own (own); auto: own at N > 1')
     ap.add_argument('--index-eqn', default='B1 - B2',
                     help='attribution runs: another index_eqn over the same two int16 bands, e.g. '
                          '"(B1 - B2) * 2 / 2" (the same values through a program that is not a '
@@ -373,7 +392,10 @@ def main():
         cfg['desc'] += ' (attribution run: trendline planes left out)'
     P = args.pixels or cfg['pixels']
     dev = torch.device('cuda', local)
-    mosaic_cfg = 'scenes' in cfg
+    mosaic_cfg = 'scenes' in cfg or args.strong
+    if args.strong and 'scenes' not in cfg:
+        cfg['scenes'] = 1
+        cfg['desc'] += ' (strong scaling: one scene, tiles round-robin over the GPUs)'
     if mosaic_cfg:  # one mosaic for the whole job, tiles round-robin over the ranks
         # four tiles per rank (at N = 8 the 32 tiles of P / 8 the round-robin was built for; at
         # N = 1 one launch per scene, as c2: 32 launches of 6.1 Mpx ran 2615 Mpx/s, each paying
@@ -531,10 +553,10 @@ def main():
         if dist is not None:
             dist.barrier()
         e2e_runner, e2e_tile = runner, mosaic.tile
-        if not mosaic_cfg and mosaic.tile > (1 << 24):
+        if mosaic.tile > (1 << 24):
             # the bands cross PCIe per tile, overlapped with the previous tile's kernels: a
             # whole-scene tile would leave the copy unhidden, so these steps use 16.8 Mpx tiles
-            m2 = Mosaic([P] * world, 1 << 24, world, rank, 'by_scene')
+            m2 = Mosaic(mosaic.scene_pixels, 1 << 24, world, rank, mosaic.assign)
             items2 = mosaic_inputs(m2, cfg['years'], cfg['k'][0], cfg['k'][1], cfg['mask'],
                                    cfg['seed'], dev, TARGET,
                                    band_layout=os.environ.get('LT_BAND_LAYOUT',
@@ -547,7 +569,17 @@ def main():
             e2e_runner.step()  # warm
             torch.cuda.synchronize()
             e2e_tile = m2.tile
-        dt, bh, bd = end_to_end(e2e_runner, cfg, args.e2e_steps)
+        labels = args.e2e_labels if args.e2e_labels != 'auto' else (
+            'own' if world > 1 else 'gather')
+        if labels == 'own' and gather:
+            # the labels stay with their ranks: a runner that exchanges nothing
+            m_e = e2e_runner.m
+            e2e_runner = MosaicRunner(eng, m_e, params, e2e_runner.items, fields, index_fn, dist,
+                                      exchange_fields=(), load_stream=not args.serial_load,
+                                      group=args.group)
+            e2e_runner.step()  # warm
+            torch.cuda.synchronize()
+        dt, bh, bd = end_to_end(e2e_runner, cfg, args.e2e_steps, labels)
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         if dist is not None:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -555,12 +587,16 @@ def main():
         e2e = {'value': round(mosaic.n_pix * args.e2e_steps / dt / 1e6, 3), 'unit': 'Mpixels/s',
                'tile_pixels': e2e_tile,
                'ms_per_step': round(dt / args.e2e_steps * 1e3, 3), 'steps': args.e2e_steps,
+               'labels': labels,
                'h2d_bytes_per_step_rank0': bh // args.e2e_steps,
                'd2h_bytes_per_step_rank0': bd // args.e2e_steps,
                'includes': 'H2D of pinned int16 bands per tile (copy stream, overlapped), '
-                           'index_eqn, analyze, label exchange, D2H of the writer\'s label '
-                           'rasters' + (' and of every per-year trendline plane per tile '
-                                        '(TrendlineStream)' if cfg['trendline'] else '')}
+                           'index_eqn, analyze, ' +
+                           ('label exchange, D2H of the writer\'s label rasters'
+                            if labels == 'gather' else
+                            'D2H of each rank\'s own label planes per tile (no exchange)') +
+                           (' and of every per-year trendline plane per tile '
+                            '(TrendlineStream)' if cfg['trendline'] else '')}
 
     # N = 1: the rate of the N > 1 pipeline on this GPU (16.8 Mpx tiles of the scene in one call,
     # per-tile completion events as the label exchange uses them), so the driver's N = 1 point and

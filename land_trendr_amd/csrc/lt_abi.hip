@@ -788,18 +788,19 @@ static int launch_tile(lt_ctx* c, const lt_params* prm, const lt_tile_in* in,
   }
   // the JIT kernels' one argument, as the product kernels get it (lt_kernels.h kernel_args)
   auto jit_launch = [&](hipFunction_t f, unsigned grid, int64_t* list,
-                        unsigned long long* counters, hipStream_t s) -> hipError_t {
+                        unsigned long long* counters, hipStream_t s, int wpb = 1) -> hipError_t {
     lt::KernelArgs a{c->d_scene, *prm, *in, *out, c->d_xtab, list, counters, yf, l.tl_bits,
                      l.tl_eqn};
     size_t sz = sizeof a;
     void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz,
                    HIP_LAUNCH_PARAM_END};
-    return hipModuleLaunchKernel(f, grid, 1, 1, 64, 1, 1, 0, s, nullptr, cfg);
+    return hipModuleLaunchKernel(f, grid, 1, 1, 64 * wpb, 1, 1, 0, s, nullptr, cfg);
   };
   // LT_SYNC_LAUNCH=1 (debugging): wait for each stage and report a fault against it
   static const bool sync_each = getenv("LT_SYNC_LAUNCH") && getenv("LT_SYNC_LAUNCH")[0] == '1';
   if (jk)
-    HIP_OR_FAIL(c, jit_launch(jk->analyze, (unsigned)nwave, dl, dn, stream));
+    HIP_OR_FAIL(c, jit_launch(jk->analyze, (unsigned)((nwave + jk->wpb - 1) / jk->wpb), dl, dn,
+                              stream, jk->wpb));
   else
     HIP_OR_FAIL(c, lt::launch_analyze(l));
   if (sync_each) HIP_OR_FAIL(c, hipStreamSynchronize(stream));

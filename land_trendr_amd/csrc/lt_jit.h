@@ -40,6 +40,7 @@ struct lt_jit_kernels {
   hipModule_t mod = nullptr;
   hipFunction_t analyze = nullptr, resolve = nullptr, resolve64 = nullptr;
   unsigned resolve_grid = 0, resolve64_grid = 0;  // resident waves of each resolve kernel
+  int wpb = 1;  // waves per workgroup of the analyze kernel (LT_JIT_WPB)
 };
 
 namespace lt_jit {
@@ -240,11 +241,20 @@ inline std::string fmt_rule(const lt_rule& r) {
 // compile-time switches, LT_JIT_WAVES the analyze kernel's occupancy): part of spec_key
 inline std::string env_switches() {
   std::string r;
-  for (const char* v : {"LT_JIT_DEFINES", "LT_JIT_WAVES", "LT_JIT_OVERRIDE_DIR"}) {
+  for (const char* v : {"LT_JIT_DEFINES", "LT_JIT_WAVES", "LT_JIT_WPB", "LT_JIT_OVERRIDE_DIR"}) {
     const char* e = getenv(v);
     r += std::string(v) + "=" + (e ? e : "") + ";";
   }
   return r;
+}
+
+// Waves per workgroup of the JIT analyze kernel (LT_JIT_WPB = 1, 2 or 4; default 1): each wave still
+// analyses its own 64 pixels with its own LDS slice; a workgroup of several takes one contiguous
+// run of 64 * wpb pixels, so its waves' pieces of each per-year row lie side by side
+inline int analyze_wpb() {
+  const char* e = getenv("LT_JIT_WPB");
+  const int w = e ? atoi(e) : 1;
+  return (w == 2 || w == 4) ? w : 1;
 }
 
 // The identity of the module source() generates for these inputs, without generating it: the
@@ -347,6 +357,8 @@ inline std::string source(const lt_index_prog& P, int maxy, int rmax, const char
   src += "__device__ inline double lt_jit_index(const LT_JIT_BAND_T* b, long long band_stride) {\n";
   src += body;
   src += "  return (double)(" + store + ");\n}\n";
+  const int wpb = analyze_wpb();
+  src += "#define LT_WPB " + std::to_string(wpb) + "\n";
   src += "#include \"lt_kernels_dev.h\"\n";
   // waves per SIMD the analyze kernel is built for (LT_JIT_WAVES, A/B runs; 4: <= 128 VGPRs)
   const char* we = getenv("LT_JIT_WAVES");
@@ -358,11 +370,11 @@ inline std::string source(const lt_index_prog& P, int maxy, int rmax, const char
          "LT_JIT_STOP_AFTER; __device__ void mark(int) const {} };\n#else\n"
          "using lt_jit_probe = lt::NoProbe;\n#endif\n";
   snprintf(k, sizeof k,
-           "extern \"C\" __global__ __launch_bounds__(64, %d) void lt_jit_analyze(const "
+           "extern \"C\" __global__ __launch_bounds__(%d, %d) void lt_jit_analyze(const "
            "lt::KernelArgs A) {\n  (void)A;\n  lt::analyze_body<%d, %d, %s, lt_jit_probe>();\n}\n"
            "extern \"C\" __global__ __launch_bounds__(64, 4) void lt_jit_resolve(const "
            "lt::KernelArgs A) {\n  (void)A;\n  lt::resolve_body<%d, %d, %s>();\n}\n",
-           waves, maxy, rmax, vt, maxy, rmax, vt);
+           64 * wpb, waves, maxy, rmax, vt, maxy, rmax, vt);
   src += k;
   // the values binary32 cannot hold: a binary64 resolve (a binary64 series uses lt_jit_resolve
   // for both lists, as the product launches its one instance twice; an int16 series has none)
@@ -500,6 +512,7 @@ inline bool load(const std::string& code, bool has_resolve64, int device, lt_jit
   };
   out.resolve_grid = grid(out.resolve);
   out.resolve64_grid = grid(out.resolve64);
+  out.wpb = analyze_wpb();  // as source() generated it (the same environment)
   return true;
 }
 

@@ -64,11 +64,17 @@ __device__ inline const KernelArgs& args() {
 // binary32, so more waves per CU), binary64 for binary64 values, else binary32 (values it cannot
 // hold defer the pixel to the binary64 resolve). Probe: lt_fast.h's phase probe (NoProbe here;
 // the profiling units of profiles/ pass theirs).
+// LT_WPB: waves per workgroup (the JIT kernels, lt_jit.h analyze_wpb; the precompiled instances 1):
+// each wave has its own LDS slice and 64 pixels; a workgroup takes 64 * LT_WPB consecutive pixels
+#ifndef LT_WPB
+#define LT_WPB 1
+#endif
 template <int MAXY, int RMAX, class VT, class Probe>
 __device__ inline void analyze_body() {
-  __shared__ WaveLds<MAXY, VT, false> L;
+  __shared__ WaveLds<MAXY, VT, false> Ls[LT_WPB];
+  WaveLds<MAXY, VT, false>& L = Ls[LT_WPB > 1 ? threadIdx.x >> 6 : 0];
   const KernelArgs& K = args();
-  const int lane = threadIdx.x;
+  const int lane = LT_WPB > 1 ? threadIdx.x & 63 : threadIdx.x;
 #ifdef LT_DEBUG_LDS_PAD
   // debugging (LT_JIT_DEFINES=LT_DEBUG_LDS_PAD=bytes): extra LDS per workgroup, to run the
   // analyze stage at a lower occupancy (fewer co-resident waves per CU) with the same code
@@ -76,7 +82,7 @@ __device__ inline void analyze_body() {
   lds_pad[lane] = (uint32_t)lane;
   asm volatile("" ::"v"(lds_pad[lane]));
 #endif
-  const int64_t p = xcd_block(blockIdx.x, gridDim.x) * 64 + lane;
+  const int64_t p = xcd_block(blockIdx.x, gridDim.x) * (64 * LT_WPB) + threadIdx.x;
   const int64_t n_pix = K.in.n_pix;
   const bool live = p < n_pix;
   const int d = analyze_fast<MAXY, RMAX, false, VT>(*K.S, K.P, K.in, K.out, K.xtab, K.yflags,

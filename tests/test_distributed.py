@@ -121,6 +121,7 @@ def test_single_process_runner_matches_oracle():
     (2, [300, 900], 256, 'by_scene', 0),     # unequal scenes (writer 2 tiles, peer 4)
     (2, [700, 300], 256, 'round_robin', 1),  # writer rank 1 (2 tiles) under round-robin (3)
     (3, [300, 200, 900], 256, 'by_scene', 2),  # writer 4 tiles, peers 2 and 1
+    (2, [1300], 256, 'round_robin', 0),      # bench --strong: ONE scene's tiles round-robin
 ])
 @pytest.mark.timeout(180)  # an unmatched send hangs: fail instead
 def test_multi_rank_exchange_matches_single_process(tmp_path, world, px, tile, assign, dst):
@@ -137,6 +138,7 @@ def test_multi_rank_exchange_matches_single_process(tmp_path, world, px, tile, a
     (2, [600, 600], 256, 'by_scene', 0),     # the c2 shape
     (2, [700, 300], 256, 'round_robin', 0),  # the c4 shape
     (3, [300, 200, 900], 256, 'by_scene', 2),  # unequal scenes, writer rank 2
+    (2, [1300], 256, 'round_robin', 0),        # bench --strong
 ])
 @pytest.mark.timeout(180)
 def test_pipelined_exchange_over_steps_matches_single_process(tmp_path, world, px, tile, assign,
@@ -235,3 +237,59 @@ def test_multi_rank_job_matches_single_rank_and_oracle(tmp_path):
 
 def _same_nan(a, b):
     return ((a.view(np.int64) == b.view(np.int64)) | (np.isnan(a) & np.isnan(b))).all()
+
+
+def _own_worker(rank, world, port, scene_px, tile, assign, result_path):
+    """bench.py's end-to-end 'own' label mode: no exchange, each rank keeps (copies to its host)
+    its own tiles' label planes; saved per tile with the tile's mosaic position."""
+    import torch.distributed as dist
+    from land_trendr_amd.engine import IndexFn
+    from land_trendr_amd.index_eqn import IndexProgram
+    from land_trendr_amd.runner import MosaicRunner
+    from land_trendr_amd.settings import compile_params
+    from land_trendr_amd.synth import mosaic_inputs
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    m = ltd.Mosaic(scene_px, tile, world, rank, assign)
+    items = mosaic_inputs(m, 20, 1, 2, 0.1, 7, 'cpu')
+    params, _ = compile_params(10, RULES)
+    fn = IndexFn(None, IndexProgram('B1 - B2', band_dtype='int16'))
+    r = MosaicRunner(OracleEngine(), m, params, items, FIELDS, fn, dist, exchange_fields=())
+    r.step()
+    r.finish()
+    assert r.exchange.full is None or not r.exchange.fields  # nothing gathered
+    out = {}
+    for k, it in enumerate(items):
+        for f in ltd.LABEL_GATHER_FIELDS:
+            out['%s:%d:%d' % (f, it.tile.g0, it.tile.n)] = r.outs[k][f][..., :it.tile.n].numpy()
+    np.savez('%s.rank%d.npz' % (result_path, rank), **out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world,px,tile,assign', [
+    (2, [600, 600], 256, 'by_scene'),  # the c2 shape
+    (2, [1300], 256, 'round_robin'),   # bench --strong
+])
+@pytest.mark.timeout(180)
+def test_own_label_planes_per_rank_match_single_process(tmp_path, world, px, tile, assign):
+    """The end-to-end 'own' label mode at N > 1 (bench.py --e2e-labels own): no
+    rank sends anything; the ranks' per-tile label planes, laid side by side by mosaic position,
+    are the single-process rasters."""
+    path = str(tmp_path / 'own')
+    mp.spawn(_own_worker, args=(world, _free_port(), px, tile, assign, path), nprocs=world,
+             join=True)
+    want = _want(px, 7)
+    got = {f: np.full(want[f][:2].shape, 7, want[f].dtype) for f in ltd.LABEL_GATHER_FIELDS}
+    seen = np.zeros(sum(px), int)
+    for rank in range(world):
+        for key, a in np.load('%s.rank%d.npz' % (path, rank)).items():
+            f, g0, n = key.split(':')
+            g0, n = int(g0), int(n)
+            got[f][..., g0:g0 + n] = a
+            if f == 'magnitude':
+                seen[g0:g0 + n] += 1
+    assert (seen == 1).all()
+    for f in ltd.LABEL_GATHER_FIELDS:
+        assert _same(want[f][:2], got[f]), f
