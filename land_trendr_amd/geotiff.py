@@ -126,11 +126,26 @@ class GeoTiff:
         except ValueError as e:
             raise TiffError(str(e))
 
-    def read(self):
-        """All bands as a [bands, rows, cols] array in the sample type (native byte order)."""
+    def read(self, threads=None, native=True):
+        """All bands as a [bands, rows, cols] array in the sample type (native byte order).
+        Strip-organised LZW / uncompressed images with integer predictors are decoded on
+        `threads` threads by liblt_io.so (default: the host's share, ingest.host_threads);
+        native=False takes the per-strip path (tests compare the two)."""
         t = self.tags
         W, H, B = self.width, self.height, self.bands
         spp = B if self.planar == 1 else 1
+        if native and 273 in t and tiffcodec.native_strips(self.compression, self.predictor, self.bits) and (
+                self.predictor == 1 or self.dtype.kind in 'iu'):
+            if threads is None:
+                from .ingest import host_threads
+                threads = host_threads()
+            rps = min(int(t.get(278, (H,))[0]), H)
+            try:
+                return tiffcodec.decode_strips(self._d, t[273], t[279], self.compression,
+                                               self.predictor, self.dtype, self._bo == '>', W, H,
+                                               B, self.planar, rps, threads)
+            except ValueError as e:
+                raise TiffError(str(e))
         if 273 in t:  # strips
             rps = min(int(t.get(278, (H,))[0]), H)
             per_band = -(-H // rps)

@@ -38,6 +38,7 @@ import sys
 import numpy as np
 
 from . import _abi
+from .geotiff import GeoTiff
 from .ingest import (analysis_rasters, grid_coords, grid_offsets, ingest_stack, mask_name,
                      rast2grid, rast_local, read_grid, stack_range)
 
@@ -105,9 +106,41 @@ class LocalJob:
             self._locate(rdir, rasts)  # every archive is extracted by now: only listed
         # the grid's point coordinates, as parsing the CSV just written gives them
         self.grid_xy = grid_coords(self.rast_fns[0])
+        self._internal_order()
         with open(self.settings_path) as f:
             self.settings = json.load(f)
         return self.rast_fns
+
+    def _internal_order(self):
+        """The job's own pixel order. rast2grid lists the template's pixels column by column
+        (utils.py:314-321) while a raster is stored row by row, so gathering every raster at the
+        grid points in grid order is a transpose of each band (a random-access gather of 49 M
+        samples per band and date). Pixels are independent and the outputs are placed by each
+        point's raster offset, so when the grid is exactly the template's pixels (the
+        co-registered stacks setup() builds) the job runs them in raster order instead: internal
+        pixel q is grid point order[q] and raster pixel q, and a raster with the template's
+        geotransform is read with a plain copy (ingest._Offsets). The grid CSV keeps the
+        reference's order; grid_wkts() gives the WKTs in the internal order."""
+        self.order = None
+        tmpl = GeoTiff(self.rast_fns[0])
+        lng, lat = self.grid_xy
+        dest, ok = grid_offsets(tmpl.geotransform(), (tmpl.height, tmpl.width), lng, lat)
+        n = tmpl.height * tmpl.width
+        if len(dest) != n or not ok.all():
+            return
+        order = np.argsort(dest, kind='stable')
+        if not np.array_equal(dest[order], np.arange(n)):  # not one point per pixel
+            return
+        if np.array_equal(order, np.arange(n)):
+            return
+        self.order = order
+        self.grid_xy = (lng[order], lat[order])
+
+    def grid_wkts(self):
+        """The grid points' WKTs in the job's internal pixel order (that of the stack and of
+        every plane): the grid CSV's order unless _internal_order() chose raster order."""
+        w = read_grid(self.grid_fn)
+        return w if self.order is None else [w[i] for i in self.order]
 
     def _locate(self, rdir, rasts):
         os.makedirs(self.work_dir, exist_ok=True)
@@ -282,7 +315,7 @@ class LocalJob:
             return
         if self.on_error == 'raise':
             p = int(bad[0])
-            wkt = read_grid(self.grid_fn)[p]
+            wkt = self.grid_wkts()[p]
             s = int(status[p])
             if s & _abi.LT_ST_PRE_THRESHOLD_ATTR:
                 raise AttributeError("LabelRule instance has no attribute 'threshold' (pixel %s)"
@@ -305,7 +338,6 @@ class LocalJob:
         finished GDT_Byte (or typed) array, written at once; a grid that maps two points to one
         pixel (the reference's loop: the last one wins) is assembled on the host."""
         import torch
-        from .geotiff import GeoTiff
         from .raster import (label_rasters, label_rasters_device, output_reducer,
                              trendline_rasters, trendline_rasters_device)
         tmpl = GeoTiff(self.rast_fns[0])
@@ -315,7 +347,7 @@ class LocalJob:
         if not ok.all():
             # data2raster assigns holder[y_off, x_off]: an off-template point raises there
             raise IndexError('grid point %s is off the template raster'
-                             % read_grid(self.grid_fn)[int(np.flatnonzero(~ok)[0])])
+                             % self.grid_wkts()[int(np.flatnonzero(~ok)[0])])
         tdt = tmpl.dtype.newbyteorder('=')
         dp = self.dev_planes
         # an EMPTY pixel never reaches the reference's reducer: it emits nothing

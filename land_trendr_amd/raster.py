@@ -157,13 +157,21 @@ def write_geotiff(path, array, template=None, nodata=NODATA, geotransform=None, 
     nb, rows, cols = a.shape
     tmpl = GeoTiff(template) if isinstance(template, str) else template
     rps = rows_per_strip or max(1, min(rows, 8192 // max(1, cols * a.dtype.itemsize)))
-    strips = []
-    for b in range(nb):
-        for y0 in range(0, rows, rps):
-            blk = a[b, y0:y0 + rps]
-            if predictor == 2:
-                blk = tiffcodec.apply_predictor2(blk, cols, 1)
-            strips.append(tiffcodec.encode(comp, np.ascontiguousarray(blk).tobytes()))
+    if tiffcodec.native_strips(comp, predictor, a.dtype.itemsize * 8):
+        # every strip on the host's threads (liblt_io.so lt_tiff_encode_strips)
+        from .ingest import host_threads
+        data, sizes = tiffcodec.encode_strips(a, rps, comp, predictor, host_threads())
+        bounds = np.concatenate([[0], np.cumsum(sizes)])
+        mv = memoryview(data)
+        strips = [mv[bounds[k]:bounds[k + 1]] for k in range(len(sizes))]
+    else:
+        strips = []
+        for b in range(nb):
+            for y0 in range(0, rows, rps):
+                blk = a[b, y0:y0 + rps]
+                if predictor == 2:
+                    blk = tiffcodec.apply_predictor2(blk, cols, 1)
+                strips.append(tiffcodec.encode(comp, np.ascontiguousarray(blk).tobytes()))
 
     def layout(data_off):
         entries = []  # (tag, type, count, payload bytes)
@@ -238,8 +246,11 @@ def write_geotiff(path, array, template=None, nodata=NODATA, geotransform=None, 
         f.write(ifd)
         f.write(extra)
         f.write(b'\x00' * (data_off - ifd_off - len(ifd) - len(extra)))
-        for st in strips:
-            f.write(st)
+        if strips and isinstance(strips[0], memoryview):  # back to back already
+            f.write(strips[0].obj[:sum(len(st) for st in strips)])
+        else:
+            for st in strips:
+                f.write(st)
     return path
 
 

@@ -26,6 +26,12 @@ def _lib():
         for f in (L.lt_lzw_decode, L.lt_lzw_encode):
             f.argtypes = [ctypes.c_char_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64]
             f.restype = ctypes.c_int64
+        i64, vp, ci = ctypes.c_int64, ctypes.c_void_p, ctypes.c_int
+        L.lt_tiff_decode_strips.argtypes = [vp, i64, vp, vp, i64, ci, ci, ci, ci, i64, i64, ci, ci,
+                                            i64, vp, ci]
+        L.lt_tiff_decode_strips.restype = i64
+        L.lt_tiff_encode_strips.argtypes = [vp, ci, i64, i64, ci, i64, ci, ci, vp, i64, vp, ci]
+        L.lt_tiff_encode_strips.restype = i64
         _LIB = L
     return _LIB
 
@@ -122,3 +128,44 @@ def apply_predictor2(block, width, spp):
     d = a.copy()
     d[:, 1:] = a[:, 1:] - a[:, :-1]  # wraps in the integer type
     return d.reshape(rows, width * spp)
+
+
+def native_strips(compression, predictor, bits):
+    """Whether lt_tiff_decode_strips / lt_tiff_encode_strips take this layout (else the
+    per-strip Python path)."""
+    return compression in (1, 5) and predictor in (1, 2) and bits in (8, 16, 32, 64)
+
+
+def decode_strips(buf, offsets, counts, compression, predictor, dtype, big_endian, width, height,
+                  bands, planar, rows_per_strip, threads):
+    """Every strip of a strip-organised image, decoded on `threads` threads (liblt_io.so
+    lt_tiff_decode_strips) -> [bands, height, width] in native byte order."""
+    out = np.empty((bands, height, width), np.dtype(dtype).newbyteorder('='))
+    offs = np.ascontiguousarray(offsets, np.uint64)
+    cnts = np.ascontiguousarray(counts, np.uint64)
+    src = np.frombuffer(buf, np.uint8)
+    rc = _lib().lt_tiff_decode_strips(src.ctypes.data, src.size, offs.ctypes.data, cnts.ctypes.data,
+                                      len(offs), compression, predictor, out.itemsize,
+                                      1 if big_endian else 0, width, height, bands, planar,
+                                      rows_per_strip, out.ctypes.data, max(1, int(threads)))
+    if rc < 0:
+        raise ValueError('TIFF strips: corrupt or unsupported data (%d)' % rc)
+    return out
+
+
+def encode_strips(a, rows_per_strip, compression, predictor, threads):
+    """[bands, rows, cols] little-endian samples -> (the strips back to back as bytes, their
+    sizes), encoded on `threads` threads (liblt_io.so lt_tiff_encode_strips)."""
+    a = np.ascontiguousarray(a)
+    nb, rows, cols = a.shape
+    n = nb * (-(-rows // rows_per_strip))
+    raw = rows * cols * a.itemsize * nb
+    cap = raw * 3 // 2 + 16 * n + 16 if compression == 5 else raw
+    out = np.empty(cap, np.uint8)
+    sizes = np.zeros(n, np.int64)
+    m = _lib().lt_tiff_encode_strips(a.ctypes.data, nb, rows, cols, a.itemsize, rows_per_strip,
+                                     compression, predictor, out.ctypes.data, cap,
+                                     sizes.ctypes.data, max(1, int(threads)))
+    if m < 0:
+        raise ValueError('TIFF strips: encode failed (%d)' % m)
+    return out[:m], sizes

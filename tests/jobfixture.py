@@ -127,7 +127,7 @@ def check_job_outputs(j, files):
     exp = oracle.analyze_tile(meta, params, expected_index(st).astype(np.float64), st['valid'])
     ok_status = (exp['status'] & ~_abi.LT_ST_EMPTY) == 0
     tmpl = GeoTiff(j.rast_fns[0])
-    want = literal_output_rasters(exp, rules, meta.dates, ingest.read_grid(j.grid_fn), tmpl,
+    want = literal_output_rasters(exp, rules, meta.dates, j.grid_wkts(), tmpl,
                                   ok_status)
     assert sorted(files) == sorted(want)
     for k, w in want.items():

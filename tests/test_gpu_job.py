@@ -47,7 +47,7 @@ def test_local_job_end_to_end(tmp_path, tile):
     # label rasters: the literal data2raster over the '<rule>_<key>' emissions of every grid point
     tmpl = GeoTiff(j.rast_fns[0])
     gt = tmpl.geotransform()
-    wkts = ingest.read_grid(j.grid_fn)
+    wkts = j.grid_wkts()  # the planes' pixel order
     ok_status = (exp['status'] & ~_abi.LT_ST_EMPTY) == 0
     for r, rule in enumerate(rules):
         for key in raster.LABEL_KEYS:

@@ -122,7 +122,7 @@ def test_ingest_stack_matches_per_point_parse(tmp_path):
     j.setup()
     assert any(m is not None for m in j.mask_fns) and any(m is None for m in j.mask_fns)
     st = j.parse()
-    wkts = ingest.read_grid(j.grid_fn)
+    wkts = j.grid_wkts()  # the job's pixel order (raster order for a co-registered grid)
     literal = _literal_parse(j, j.rast_fns, j.mask_fns, j.grid_fn)
     idx = (st['bands'][:, 0, :].astype(np.int32) - st['bands'][:, 1, :]).astype(np.int16)
     n_dropped = 0
@@ -147,13 +147,16 @@ def test_grid_coords_equal_parsing_the_written_grid(tmp_path):
     make_job(root)
     j = LocalJob(root, 'synth')
     j.setup()
+    order = j.order if j.order is not None else slice(None)
     for a, b in zip(j.grid_xy, ingest.grid_points(j.grid_fn)):
-        assert np.array_equal(a.view(np.int64), b.view(np.int64))
+        assert np.array_equal(a.view(np.int64), b[order].view(np.int64))
+    assert j.order is not None  # the fixture's grid is its template's pixels: raster order
     # the threaded ingest from coordinates equals a serial one from the CSV
     st = ingest.ingest_stack(j.rast_fns, j.grid_xy, j.mask_fns, bands=[1, 2])
     st1 = ingest.ingest_stack(j.rast_fns, j.grid_fn, j.mask_fns, bands=[1, 2], threads=1)
     assert st['dates'] == st1['dates']
-    assert np.array_equal(st['bands'], st1['bands']) and np.array_equal(st['valid'], st1['valid'])
+    assert np.array_equal(st['bands'], st1['bands'][..., order])
+    assert np.array_equal(st['valid'], st1['valid'][..., order])
     # a rank's share (pixel ranges): exactly those columns, back to back; stack_range finds them
     P = st['n_pix']
     spans = [(0, 7), (P // 2, P // 2 + 13), (P - 5, P)]

@@ -140,3 +140,103 @@ def test_floating_point_predictor_undo_with_chunky_bands(spp, dtype):
     got = tiffcodec.undo_predictor(block.copy(), 3, np.dtype('<' + np.dtype(dtype).str[1:]),
                                    width, spp)
     assert np.array_equal(got.astype(dtype), a)
+
+
+def _strip_tiff(path, a, bo='<', planar=2, predictor=1, compression=5, rps=3):
+    """A strip TIFF written by hand (any byte order, chunky or planar, predictor 2), the reader's
+    reference being its own per-strip path."""
+    import struct
+    from land_trendr_amd import tiffcodec
+    nb, rows, cols = a.shape
+    a = a.astype(a.dtype.newbyteorder(bo))
+    strips = []
+    if planar == 2:
+        blocks = [a[b, y:y + rps] for b in range(nb) for y in range(0, rows, rps)]
+        spp = 1
+    else:
+        blocks = [a[:, y:y + rps].transpose(1, 2, 0) for y in range(0, rows, rps)]
+        spp = nb
+    for blk in blocks:
+        blk = np.ascontiguousarray(blk).reshape(blk.shape[0], -1)
+        if predictor == 2:
+            nat = blk.astype(blk.dtype.newbyteorder('='))
+            d = nat.reshape(blk.shape[0], cols, spp).copy()
+            d[:, 1:] = d[:, 1:] - d[:, :-1]
+            blk = d.reshape(blk.shape).astype(blk.dtype)
+        strips.append(tiffcodec.encode(compression, np.ascontiguousarray(blk).tobytes()))
+    tags = [(256, 4, [cols]), (257, 4, [rows]), (258, 3, [a.dtype.itemsize * 8] * nb),
+            (259, 3, [compression]), (262, 3, [1]), (273, 4, None), (277, 3, [nb]),
+            (278, 4, [rps]), (279, 4, [len(s) for s in strips]), (284, 3, [planar]),
+            (317, 3, [predictor]), (339, 3, [2 if a.dtype.kind == 'i' else 1] * nb)]
+    fmt = {3: 'H', 4: 'I'}
+    n = len(tags)
+    extra_off = 8 + 2 + 12 * n + 4
+    payloads = {}
+    extra = b''
+    data_off = extra_off + 4096
+    offs, o = [], data_off
+    for st in strips:
+        offs.append(o)
+        o += len(st)
+    ifd = struct.pack(bo + 'H', n)
+    for tag, typ, vals in tags:
+        if vals is None:
+            vals = offs
+        payload = struct.pack(bo + fmt[typ] * len(vals), *vals)
+        if len(payload) <= 4:
+            ifd += struct.pack(bo + 'HHI', tag, typ, len(vals)) + payload.ljust(4, b'\x00')
+        else:
+            ifd += struct.pack(bo + 'HHII', tag, typ, len(vals), extra_off + len(extra))
+            extra += payload
+    ifd += struct.pack(bo + 'I', 0)
+    assert len(extra) <= 4096
+    with open(path, 'wb') as f:
+        f.write((b'II' if bo == '<' else b'MM') + struct.pack(bo + 'HI', 42, 8))
+        f.write(ifd)
+        f.write(extra.ljust(4096, b'\x00'))
+        for st in strips:
+            f.write(st)
+
+
+@pytest.mark.parametrize('dtype,bo,planar,predictor,compression', [
+    (np.int16, '<', 2, 1, 5), (np.int16, '>', 2, 2, 5), (np.uint16, '<', 1, 2, 5),
+    (np.int32, '>', 1, 1, 1), (np.uint8, '<', 2, 2, 5), (np.int16, '<', 1, 1, 1)])
+def test_native_strip_decode_matches_per_strip_path(tmp_path, dtype, bo, planar, predictor,
+                                                   compression):
+    """liblt_io.so lt_tiff_decode_strips (threads, byte swap, predictor 2, chunky de-interleave,
+    a short last strip) reads what the per-strip path reads."""
+    from land_trendr_amd.geotiff import GeoTiff
+    rng = np.random.default_rng(3)
+    a = rng.integers(-3000 if np.dtype(dtype).kind == 'i' else 0, 3000, (3, 11, 7)).astype(dtype)
+    p = str(tmp_path / 'x.tif')
+    _strip_tiff(p, a, bo, planar, predictor, compression, rps=4)
+    g = GeoTiff(p)
+    want = g.read(native=False)
+    assert np.array_equal(want, a)
+    for threads in (1, 3):
+        got = g.read(threads=threads)
+        assert got.dtype == want.dtype and np.array_equal(got, want)
+
+
+def test_native_strip_encode_matches_per_strip_encoder(tmp_path):
+    """write_geotiff's threaded strips (lt_tiff_encode_strips) are byte for byte the per-strip
+    encoder's, and read back."""
+    from land_trendr_amd import tiffcodec
+    from land_trendr_amd.geotiff import GeoTiff
+    from land_trendr_amd.raster import write_geotiff
+    rng = np.random.default_rng(4)
+    a = rng.integers(-500, 500, (2, 37, 29)).astype(np.int16)
+    for predictor in (1, 2):
+        data, sizes = tiffcodec.encode_strips(a, 5, 5, predictor, 3)
+        ref = []
+        for b in range(2):
+            for y in range(0, 37, 5):
+                blk = a[b, y:y + 5]
+                if predictor == 2:
+                    blk = tiffcodec.apply_predictor2(blk, 29, 1)
+                ref.append(tiffcodec.encode(5, np.ascontiguousarray(blk).tobytes()))
+        assert list(sizes) == [len(r) for r in ref]
+        assert data.tobytes() == b''.join(ref)
+        p = str(tmp_path / ('p%d.tif' % predictor))
+        write_geotiff(p, a, predictor=predictor, rows_per_strip=5)
+        assert np.array_equal(GeoTiff(p).read(), a)
