@@ -17,7 +17,8 @@ extern "C" {
 
 enum { LT_IO_ERR_ARG = -1, LT_IO_ERR_DATA = -2, LT_IO_ERR_SPACE = -3 };
 
-/* One TIFF LZW strip or tile (Compression = 5) -> its raw bytes (at most cap). */
+/* One TIFF LZW strip or tile (Compression = 5) -> its raw bytes (at most cap; bytes of out past
+ * the returned count may be overwritten, never past cap). */
 int64_t lt_lzw_decode(const uint8_t* in, int64_t n_in, uint8_t* out, int64_t cap);
 /* Raw bytes -> one TIFF LZW strip (libtiff's code stream: Clear first, 9..12-bit codes, early
  * change, Clear when the table is full). cap >= n_in * 3 / 2 + 16 always suffices. */

@@ -54,81 +54,121 @@ extern "C" {
 
 int64_t lt_lzw_decode(const uint8_t* in, int64_t n_in, uint8_t* out, int64_t cap) {
   if (!in || n_in < 0 || (cap > 0 && !out)) return LT_IO_ERR_ARG;
-  // string table: prefix code, last byte, length, first byte
-  static thread_local uint16_t prefix[4096];
-  static thread_local uint8_t last[4096], first[4096];
-  static thread_local uint16_t len[4096];
-  for (int c = 0; c < 256; c++) {
-    prefix[c] = 0xFFFF;
-    last[c] = first[c] = (uint8_t)c;
-    len[c] = 1;
-  }
-  int nbits = 9, free_ent = kFirst, old = -1;
-  int64_t n_out = 0, byte_pos = 0;
-  // bit reader: whole bytes into a 64-bit buffer, codes taken from its top (MSB first); a code
-  // the remaining input cannot fill ends the strip
-  uint64_t bitbuf = 0;
-  int nbuf = 0;
-  auto get = [&](int nb) -> int {
-    while (nbuf < nb) {
-      if (byte_pos >= n_in) return -1;
-      bitbuf = (bitbuf << 8) | in[byte_pos++];
-      nbuf += 8;
+  if (cap >= (int64_t)1 << 31) return LT_IO_ERR_ARG;  // strips are far smaller (32-bit positions)
+  // Every string of the table is already in `out`: code c >= kFirst is the len[c] bytes at
+  // out[pos[c]] (where it was last written), so emitting is a copy from earlier output and a new
+  // entry is (the previous emission's position, its length + 1): no per-byte chain walk. The
+  // table lives on the stack (a thread_local one in a -fPIC library costs a __tls_get_addr call
+  // per access).
+  uint32_t pos[4096];
+  uint16_t len[4096];
+  int nbits = 9, free_ent = kFirst;
+  uint32_t mask = (1u << 9) - 1u;
+  int64_t n_out = 0;
+  int64_t bitpos = 0;
+  const int64_t nbits_in = n_in * 8;
+  const int64_t fast_end = (n_in - 4) * 8;  // a 32-bit load at bitpos >> 3 stays inside `in`
+  // the next code (MSB first): one unaligned big-endian 32-bit load while 4 bytes remain, else a
+  // byte at a time; -1 when the input cannot fill a whole code (the strip's end)
+  auto get = [&]() -> int {
+    if (bitpos <= fast_end) {
+      uint32_t w;
+      memcpy(&w, in + (bitpos >> 3), 4);
+      w = __builtin_bswap32(w);
+      const int code = (int)((w >> (32 - nbits - (int)(bitpos & 7))) & mask);
+      bitpos += nbits;
+      return code;
     }
-    nbuf -= nb;
-    return (int)((bitbuf >> nbuf) & ((1u << nb) - 1u));
+    if (bitpos + nbits > nbits_in) return -1;
+    uint32_t acc = 0;
+    for (int k = 0; k < nbits; k++, bitpos++)
+      acc = (acc << 1) | ((in[bitpos >> 3] >> (7 - (bitpos & 7))) & 1u);
+    return (int)acc;
   };
-  auto emit = [&](int code) -> bool {
-    const int L = len[code];
-    if (n_out + L > cap) return false;
-    int c = code;
-    for (int k = L - 1; k >= 0; k--) {
-      out[n_out + k] = last[c];
-      c = prefix[c];
+  uint32_t old_pos = 0;  // the previous code's emission
+  int old_len = 0;
+  // copy L bytes from out[src] (src + L <= dst: earlier output, no overlap) to out[dst]
+  auto copy = [&](uint8_t* dst, const uint8_t* src, int L) {
+    if (L <= 16 && dst + 16 <= out + cap) {  // two unaligned 8-byte moves (the slack is output
+      uint64_t a, b;                          // space later codes overwrite)
+      memcpy(&a, src, 8);
+      memcpy(&b, src + 8, 8);
+      memcpy(dst, &a, 8);
+      if (L > 8) memcpy(dst + 8, &b, 8);
+    } else {
+      for (int k = 0; k < L; k++) dst[k] = src[k];
     }
-    n_out += L;
-    return true;
   };
+  bool have_old = false;
   for (;;) {
-    int code = get(nbits);
+    int code = get();
     if (code < 0 || code == kEoi) break;  // a strip may end without EOI (libtiff tolerates it)
     if (code == kClear) {
       nbits = 9;
+      mask = (1u << 9) - 1u;
       free_ent = kFirst;
-      code = get(nbits);
+      code = get();
       if (code < 0 || code == kEoi) break;
       if (code >= 256) return LT_IO_ERR_DATA;
-      if (!emit(code)) return LT_IO_ERR_SPACE;
-      old = code;
+      if (n_out >= cap) return LT_IO_ERR_SPACE;
+      out[n_out] = (uint8_t)code;
+      old_pos = (uint32_t)n_out++;
+      old_len = 1;
+      have_old = true;
       continue;
     }
-    if (old < 0) {  // data must start with a Clear code or a literal
+    if (!have_old) {  // data must start with a Clear code or a literal
       if (code >= 256) return LT_IO_ERR_DATA;
-      if (!emit(code)) return LT_IO_ERR_SPACE;
-      old = code;
+      if (n_out >= cap) return LT_IO_ERR_SPACE;
+      out[n_out] = (uint8_t)code;
+      old_pos = (uint32_t)n_out++;
+      old_len = 1;
+      have_old = true;
       continue;
     }
-    if (code < free_ent && code != kClear && code != kEoi) {
-      if (!emit(code)) return LT_IO_ERR_SPACE;
-      if (free_ent < 4096) {
-        prefix[free_ent] = (uint16_t)old;
-        last[free_ent] = first[code];
-        first[free_ent] = first[old];
-        len[free_ent] = (uint16_t)(len[old] + 1);
+    if (code < 256) {  // a literal
+      if (n_out >= cap) return LT_IO_ERR_SPACE;
+      out[n_out] = (uint8_t)code;
+      if (free_ent < 4096) {  // previous string + this byte: contiguous in out
+        pos[free_ent] = old_pos;
+        len[free_ent] = (uint16_t)(old_len + 1);
         free_ent++;
       }
+      old_pos = (uint32_t)n_out++;
+      old_len = 1;
+    } else if (code < free_ent) {
+      const int L = len[code];
+      if (n_out + L > cap) return LT_IO_ERR_SPACE;
+      copy(out + n_out, out + pos[code], L);
+      if (free_ent < 4096) {
+        pos[free_ent] = old_pos;
+        len[free_ent] = (uint16_t)(old_len + 1);
+        free_ent++;
+      }
+      old_pos = (uint32_t)n_out;
+      old_len = L;
+      n_out += L;
     } else if (code == free_ent && free_ent < 4096) {
-      prefix[free_ent] = (uint16_t)old;
-      last[free_ent] = first[old];
-      first[free_ent] = first[old];
-      len[free_ent] = (uint16_t)(len[old] + 1);
+      // KwKwK: the previous string + its own first byte
+      const int L = old_len + 1;
+      if (n_out + L > cap) return LT_IO_ERR_SPACE;
+      uint8_t* dst = out + n_out;
+      const uint8_t* src = out + old_pos;
+      copy(dst, src, old_len);
+      dst[old_len] = src[0];
+      pos[free_ent] = (uint32_t)n_out;
+      len[free_ent] = (uint16_t)L;
       free_ent++;
-      if (!emit(code)) return LT_IO_ERR_SPACE;
+      old_pos = (uint32_t)n_out;
+      old_len = L;
+      n_out += L;
     } else {
       return LT_IO_ERR_DATA;
     }
-    old = code;
-    if (free_ent >= (1 << nbits) - 1 && nbits < kMaxBits) nbits++;
+    if (free_ent >= (1 << nbits) - 1 && nbits < kMaxBits) {
+      nbits++;
+      mask = (1u << nbits) - 1u;
+    }
   }
   return n_out;
 }
@@ -138,12 +178,22 @@ int64_t lt_lzw_encode(const uint8_t* in, int64_t n_in, uint8_t* out, int64_t cap
   BitWriter w{out, cap};
   // child lookup: (code, byte) -> code in a 4096 x 256 table; an entry is valid only if its
   // generation is the current one, so a table reset (Clear) is one increment, not a 2 MB fill
-  static thread_local std::vector<uint16_t> next((size_t)4096 * 256, 0);
-  static thread_local std::vector<uint32_t> gen((size_t)4096 * 256, 0);
-  static thread_local uint32_t cur = 0;
+  static thread_local std::vector<uint16_t> next_tl((size_t)4096 * 256, 0);
+  static thread_local std::vector<uint32_t> gen_tl((size_t)4096 * 256, 0);
+  static thread_local uint32_t cur_tl = 0;
+  // one TLS lookup per call, not per byte (a thread_local access in a -fPIC library is a
+  // __tls_get_addr call)
+  uint16_t* const next = next_tl.data();
+  uint32_t* const gen = gen_tl.data();
+  uint32_t cur = cur_tl;
+  struct Keep {
+    uint32_t& dst;
+    uint32_t& src;
+    ~Keep() { dst = src; }
+  } keep{cur_tl, cur};
   auto fresh = [&]() {
     if (++cur == 0) {  // wrapped: start over
-      std::fill(gen.begin(), gen.end(), 0u);
+      std::fill(gen, gen + (size_t)4096 * 256, 0u);
       cur = 1;
     }
   };

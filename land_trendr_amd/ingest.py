@@ -150,6 +150,14 @@ def grid_wkts(ds):
     return ['POINT(%s %s)' % (a, b) for a in xt for b in yt]
 
 
+def grid_axes(ds):
+    """The grid's distinct coordinates as grid_coords parses them: (x of each raster column,
+    y of each raster row)."""
+    xt, yt = _grid_text(ds)
+    return (np.array([float(t) for t in xt], np.float64),
+            np.array([float(t) for t in yt], np.float64))
+
+
 def grid_coords(ds):
     """grid_points of the grid rast2grid writes for raster `ds`, without the text round trip per
     point: each distinct coordinate text (one per column and per row) is parsed once, as OGR /
@@ -259,16 +267,21 @@ def host_threads():
 class _Offsets:
     """grid_offsets per distinct (geotransform, shape), computed once (a stack's rasters nearly
     all share one), with whether the grid is the raster's own pixels in order (then sampling is
-    a plain copy)."""
+    a plain copy). raster_grid = (geotransform, rows, cols): the caller knows the grid is exactly
+    that raster's pixels in raster order (LocalJob._internal_order), so a raster of that
+    geotransform and shape is a copy without computing 49 M offsets."""
 
-    def __init__(self, lng, lat):
+    def __init__(self, lng, lat, raster_grid=None):
         import threading
         self.lng, self.lat = lng, lat
+        self.raster_grid = raster_grid
         self.cache = {}
         self.lock = threading.Lock()
 
     def __call__(self, ds):
         key = (ds.geotransform(), ds.height, ds.width)
+        if self.raster_grid is not None and key == tuple(self.raster_grid):
+            return None, None, True
         with self.lock:
             hit = self.cache.get(key)
             if hit is None:
@@ -279,7 +292,8 @@ class _Offsets:
         return hit
 
 
-def ingest_stack(rast_fns, grid, mask_fns=None, bands=None, threads=None, pixels=None):
+def ingest_stack(rast_fns, grid, mask_fns=None, bands=None, threads=None, pixels=None,
+                 raster_grid=None):
     """parse_mapper over every analysis raster, as planes for analysis_reducer_batch.
 
     rast_fns: the (decompressed) analysis rasters, in the mapper order that becomes each pixel's
@@ -293,7 +307,9 @@ def ingest_stack(rast_fns, grid, mask_fns=None, bands=None, threads=None, pixels
     rank keeps the pixel columns its tiles analyse).
     Returns dict(dates=['YYYY-MM-DD'] * K, bands=[K, nb, Q] in the rasters' sample type,
     band_numbers=[nb], valid=[K, Q] uint8, n_pix=P, ranges=[(p0, p1, q0)]) with Q the points
-    gathered; grid point p of range (p0, p1, q0) is column q0 + p - p0 (stack_range)."""
+    gathered; grid point p of range (p0, p1, q0) is column q0 + p - p0 (stack_range).
+    raster_grid: (geotransform, rows, cols) when grid point p is pixel p of such a raster (the
+    job's raster order): rasters of that georeferencing are read by slicing, not by offsets."""
     from concurrent.futures import ThreadPoolExecutor
     lng, lat = grid if isinstance(grid, tuple) else grid_points(grid)
     P = len(lng)
@@ -322,8 +338,22 @@ def ingest_stack(rast_fns, grid, mask_fns=None, bands=None, threads=None, pixels
     dtype = first.dtype.newbyteorder('=')
     out_bands = np.empty((K, len(numbers), Q), dtype)
     valid = np.empty((K, Q), np.uint8)
-    offsets = _Offsets(lng, lat)
+    offsets = _Offsets(lng, lat, raster_grid)
     sel = [b - 1 for b in numbers]
+    spans = [(p0, p1, q0) for p0, p1, q0 in ranges]
+
+    def take(flat, idx, ok, ident, out):
+        """Samples of the gathered grid points from a raster's flat [..., H*W] samples."""
+        if ident and idx is None:  # raster order: the pixel ranges themselves
+            if len(spans) == 1 and spans[0][:2] == (0, P) and flat.shape[-1] == P:
+                out[...] = flat
+            else:
+                for p0, p1, q0 in spans:
+                    out[..., q0:q0 + p1 - p0] = flat[..., p0:p1]
+        elif ident:
+            out[...] = flat
+        else:
+            np.take(flat, idx, axis=-1, out=out)
 
     def one(k):
         fn = rast_fns[k]
@@ -333,24 +363,30 @@ def ingest_stack(rast_fns, grid, mask_fns=None, bands=None, threads=None, pixels
         if max(numbers) > ds.bands:
             raise Exception('Band %s requested but raster only has %s bands' % (max(numbers),
                                                                                  ds.bands))
-        planes = ds.read().reshape(ds.bands, -1)
+        planes = ds.read(threads=per_file).reshape(ds.bands, -1)
         idx, ok, ident = offsets(ds)
-        if ident:  # the grid is this raster's pixels in order: a copy
-            out_bands[k] = planes[sel]
-        else:
-            np.take(planes[sel], idx, axis=1, out=out_bands[k])
+        src = planes[sel] if sel != list(range(ds.bands)) else planes
+        take(src, idx, ok, ident, out_bands[k])
+        if ok is not None and not ident:
             out_bands[k][:, ~ok] = 0
-        v = ok.astype(np.uint8)
+        v = valid[k]
+        v[...] = 1 if ok is None else ok
         if mask_fns[k]:
             mds = _open(mask_fns[k])
             midx, mok, mident = offsets(mds)
-            m = mds.read()[0].reshape(-1)
-            mval = m if mident else m[midx]
-            v &= ~(mok & (mval == 0))
-        valid[k] = v
+            m = mds.read(threads=per_file)[0].reshape(-1)
+            mval = np.empty(Q, m.dtype)
+            take(m, midx, mok, mident, mval)
+            drop = (mval == 0) if mok is None else (mok & (mval == 0))
+            v &= ~drop
         return filename2date(fn)
 
-    n = max(1, min(K, threads or host_threads()))
+    total = threads or host_threads()
+    # a few files at a time, each file's strips on its share of the threads (lt_tiff_decode_strips
+    # balances thousands of strips; one thread per file left half the workers idle in the last
+    # round of a 30-file stack)
+    n = max(1, min(K, total, max(1, total // 4)))
+    per_file = max(1, total // n)
     with ThreadPoolExecutor(n) as pool:
         dates = list(pool.map(one, range(K)))
     return dict(dates=dates, bands=out_bands, band_numbers=numbers, valid=valid, n_pix=P,

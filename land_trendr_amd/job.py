@@ -39,8 +39,8 @@ import numpy as np
 
 from . import _abi
 from .geotiff import GeoTiff
-from .ingest import (analysis_rasters, grid_coords, grid_offsets, ingest_stack, mask_name,
-                     rast2grid, rast_local, read_grid, stack_range)
+from .ingest import (analysis_rasters, grid_axes, grid_coords, grid_offsets, ingest_stack,
+                     mask_name, rast2grid, rast_local, read_grid, stack_range)
 
 IN_SETTINGS = '%s/input/settings.json'
 IN_RASTS = '%s/input/rasters/'
@@ -69,6 +69,8 @@ class LocalJob:
         self.engine = engine
         self._host = None
         self.host_trendline = None
+        self.order = None        # grid point of each internal pixel (None: grid order)
+        self.raster_grid = None  # (geotransform, rows, cols) of the raster order, or None
 
     def _path(self, key):
         return os.path.join(self.root, key)
@@ -116,25 +118,27 @@ class LocalJob:
         (utils.py:314-321) while a raster is stored row by row, so gathering every raster at the
         grid points in grid order is a transpose of each band (a random-access gather of 49 M
         samples per band and date). Pixels are independent and the outputs are placed by each
-        point's raster offset, so when the grid is exactly the template's pixels (the
-        co-registered stacks setup() builds) the job runs them in raster order instead: internal
-        pixel q is grid point order[q] and raster pixel q, and a raster with the template's
-        geotransform is read with a plain copy (ingest._Offsets). The grid CSV keeps the
-        reference's order; grid_wkts() gives the WKTs in the internal order."""
+        point's raster offset, so when every grid point lands on its own template pixel (the
+        co-registered grid setup() builds from the template) the job runs them in raster order
+        instead: internal pixel q is raster pixel q and grid point order[q], and a raster with the
+        template's georeferencing is read by slicing (ingest_stack raster_grid). The check is
+        pt2val's addressing (grid_offsets' operations) on the grid's distinct coordinates: the
+        offsets of a column's points depend on its x alone, a row's on its y. The grid CSV keeps
+        the reference's order; grid_wkts() gives the WKTs in the internal order."""
         self.order = None
+        self.raster_grid = None
         tmpl = GeoTiff(self.rast_fns[0])
-        lng, lat = self.grid_xy
-        dest, ok = grid_offsets(tmpl.geotransform(), (tmpl.height, tmpl.width), lng, lat)
-        n = tmpl.height * tmpl.width
-        if len(dest) != n or not ok.all():
-            return
-        order = np.argsort(dest, kind='stable')
-        if not np.array_equal(dest[order], np.arange(n)):  # not one point per pixel
-            return
-        if np.array_equal(order, np.arange(n)):
-            return
-        self.order = order
-        self.grid_xy = (lng[order], lat[order])
+        H, W = tmpl.height, tmpl.width
+        gt = tmpl.geotransform()
+        xv, yv = grid_axes(tmpl)
+        xo = np.trunc((xv - gt[0]) * 1.0 / gt[1])
+        yo = np.trunc((yv - gt[3]) * 1.0 / gt[5])
+        if not (np.array_equal(xo, np.arange(W)) and np.array_equal(yo, np.arange(H))):
+            return  # some point not on its own pixel: grid order, offsets per point
+        q = np.arange(H * W, dtype=np.int64)
+        self.order = (q % W) * H + q // W  # pixel (row r, column c) is grid point c * H + r
+        self.grid_xy = (np.tile(xv, H), np.repeat(yv, W))
+        self.raster_grid = (gt, H, W)
 
     def grid_wkts(self):
         """The grid points' WKTs in the job's internal pixel order (that of the stack and of
@@ -165,7 +169,8 @@ class LocalJob:
         self.mosaic = Mosaic([P], self.tile_pixels, world, rank, 'round_robin')
         eqn_bands = sorted(parse_eqn_bands(self.settings['index_eqn']))
         self.stack = ingest_stack(self.rast_fns, self.grid_xy, self.mask_fns, bands=eqn_bands,
-                                  pixels=[(t.p0, t.p1) for t in self.mosaic.mine])
+                                  pixels=[(t.p0, t.p1) for t in self.mosaic.mine],
+                                  raster_grid=self.raster_grid)
         return self.stack
 
     # 3. analysis_reducer, batched over pixel tiles: the mosaic path (runner.py) bench.py runs
@@ -343,7 +348,10 @@ class LocalJob:
         tmpl = GeoTiff(self.rast_fns[0])
         rows, cols = tmpl.height, tmpl.width
         lng, lat = self.grid_xy
-        dest, ok = grid_offsets(tmpl.geotransform(), (rows, cols), lng, lat)
+        if self.order is not None:  # raster order: internal pixel q is template pixel q
+            dest, ok = np.arange(rows * cols, dtype=np.int64), np.ones(rows * cols, bool)
+        else:
+            dest, ok = grid_offsets(tmpl.geotransform(), (rows, cols), lng, lat)
         if not ok.all():
             # data2raster assigns holder[y_off, x_off]: an off-template point raises there
             raise IndexError('grid point %s is off the template raster'
@@ -356,7 +364,8 @@ class LocalJob:
         self._host = None
         names = [d.strftime('%Y-%m-%d') for d in self.scene.dates]
         cuda = torch.device(self.engine.device).type == 'cuda'
-        if cuda and len(np.unique(dest)) == len(dest) and len(set(names)) == len(names):
+        distinct = self.order is not None or np.bincount(dest, minlength=rows * cols).max() <= 1
+        if cuda and distinct and len(set(names)) == len(names):
             ddest = torch.from_numpy(np.ascontiguousarray(dest, np.int64)).to(dp['status'].device)
             out = {}
 

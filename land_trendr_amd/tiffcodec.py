@@ -42,6 +42,7 @@ def lzw_decode(data, size):
     n = _lib().lt_lzw_decode(bytes(data), len(data), out.ctypes.data, size)
     if n < 0:
         raise ValueError('LZW: corrupt strip (%d)' % n)
+    out[n:] = 0  # (the decoder may leave scratch bytes past the end of a short strip)
     return out
 
 
