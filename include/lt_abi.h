@@ -388,7 +388,11 @@ int lt_ctx_jit_stats(lt_ctx* ctx, lt_jit_stats* out, char* last_error, int64_t c
  * `prog` (masked: the tile has a cloud mask; year_out: a per-year plane is requested), with the
  * launch constants (LT_JIT_SRC_SPEC) and the scene's tables (LT_JIT_SRC_SCENE); host only, for
  * inspection and ahead-of-time builds. Returns the length, or a negative LT_ERR_*. */
-enum { LT_JIT_SRC_SPEC = 1, LT_JIT_SRC_SCENE = 2 };
+enum { LT_JIT_SRC_SPEC = 1, LT_JIT_SRC_SCENE = 2, LT_JIT_SRC_FIELDS = 4 };
+/* LT_JIT_SRC_FIELDS: flags bits 8.. carry the launch's non-null output planes as the kernels'
+ * LT_FIELD_* bits (status 0, n_years 1, matched 2, class_val 3, onset_year 4, duration 5,
+ * magnitude 6, initial_val 7, winner 8, val_raw 9, val_fit 10, fit_m 11, fit_b 12, right_m 13,
+ * right_b 14, spike 15, vertex 16), as the context specialises a launch for them. */
 int lt_jit_source(const lt_scene* scene, const lt_params* params, const lt_index_prog* prog,
                   int32_t masked, int32_t year_out, int32_t flags, char* buf, int64_t cap);
 

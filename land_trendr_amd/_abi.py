@@ -185,7 +185,12 @@ EXPORTS = ['lt_abi_version', 'lt_ctx_create', 'lt_ctx_destroy', 'lt_last_error',
            'lt_jit_source', 'lt_analyze_tiles_ev']
 
 LT_JIT_SYNC, LT_JIT_ASYNC = 0, 1
-LT_JIT_SRC_SPEC, LT_JIT_SRC_SCENE = 1, 2
+LT_JIT_SRC_SPEC, LT_JIT_SRC_SCENE, LT_JIT_SRC_FIELDS = 1, 2, 4
+# the kernels' output-plane bits (lt_pixel.h LT_FIELD_*), for LT_JIT_SRC_FIELDS
+LT_FIELD_BITS = {f: 1 << k for k, f in enumerate((
+    'status', 'n_years', 'matched', 'class_val', 'onset_year', 'duration', 'magnitude',
+    'initial_val', 'winner', 'val_raw', 'val_fit', 'fit_m', 'fit_b', 'right_m', 'right_b',
+    'spike', 'vertex'))}
 
 
 class LtJitStats(ctypes.Structure):

@@ -585,6 +585,13 @@ static int jit_acquire(lt_ctx* c, const lt_index* f, int Y, const lt_params* prm
     sp.tl_split = tl_split_launch(c, o);
     sp.params = *prm;
     if (scene_on) sp.scene = scene;
+    // the launch's output planes as constants (LT_JIT_FIELDS=0: read at run time, A/B;
+    // LT_JIT_FIELDS_OR=hex: planes also treated as present, A/B of which dropped plane matters)
+    static const bool fields_on = !(getenv("LT_JIT_FIELDS") && getenv("LT_JIT_FIELDS")[0] == '0');
+    static const uint32_t fields_or =
+        getenv("LT_JIT_FIELDS_OR") ? (uint32_t)strtoul(getenv("LT_JIT_FIELDS_OR"), nullptr, 16) : 0u;
+    sp.fields_on = fields_on;
+    sp.fields = fields_on ? lt_jit::spec_fields(lt_jit::out_field_mask(o) | fields_or, rmax) : 0u;
   }
   uint64_t key = lt_jit::spec_key(f->prog, maxy, rmax, vt, sp);
   auto it = c->jit.find(key);
@@ -1210,6 +1217,10 @@ int lt_jit_source(const lt_scene* sc, const lt_params* prm, const lt_index_prog*
     sp.tl_split = sp.year_out && getenv("LT_TL_SPLIT") && getenv("LT_TL_SPLIT")[0] == '1';
     sp.params = *prm;
     if (flags & LT_JIT_SRC_SCENE) sp.scene = &tmp;
+    if (flags & LT_JIT_SRC_FIELDS) {  // the output-field mask in bits 8.. of flags
+      sp.fields_on = true;
+      sp.fields = lt_jit::spec_fields((uint32_t)flags >> 8, rmax);
+    }
   }
   std::string err;
   const char* vt = lt_jit::series_type(prog->out_type, n_rules);

@@ -471,7 +471,7 @@ __device__ inline int analyze_fast(const DevScene& S_launch, const lt_params& P,
         // labels-only int16 series, branch-free: every lane takes the step; a lane without the
         // year (or dead) writes slot T (its next point overwrites it; past its series it is never
         // read) and keeps T and the sums (c2 +1.4 %, c3 +1.1 %, profiles/r05_run29)
-        if (!out.winner && !out.val_raw) {  // launch-uniform
+        if (!LT_OUTF(out, winner) && !LT_OUTF(out, val_raw)) {  // launch-uniform
           const bool pr = live && best[u] >= 0;
           if ((S.feb29_mask >> y) & 1) status |= pr ? LT_ST_FEB29 : 0;
           const double v = val[u];
@@ -489,8 +489,8 @@ __device__ inline int analyze_fast(const DevScene& S_launch, const lt_params& P,
       }
       if (!live) continue;
       const int64_t q = (int64_t)y * os + p;
-      if (out.winner && LT_AB_NO_YEAR_STORES < 2)
-        __builtin_nontemporal_store((int16_t)best[u], out.winner + q);
+      if (LT_OUTF(out, winner) && LT_AB_NO_YEAR_STORES < 2)
+        __builtin_nontemporal_store((int16_t)best[u], LT_OUTF(out, winner) + q);
       if (best[u] >= 0) {
         if ((S.feb29_mask >> y) & 1) status |= LT_ST_FEB29;
         const double v = val[u];
@@ -514,9 +514,10 @@ __device__ inline int analyze_fast(const DevScene& S_launch, const lt_params& P,
         }
         pres |= 1ull << y;
         T++;
-        if (out.val_raw && LT_AB_NO_YEAR_STORES < 2) year_row_store(v, out.val_raw + q);
-      } else if (out.val_raw && LT_AB_NO_YEAR_STORES < 2) {  // the other per-year planes: the year-major output loop
-        __builtin_nontemporal_store(nan, out.val_raw + q);
+        if (LT_OUTF(out, val_raw) && LT_AB_NO_YEAR_STORES < 2)
+          year_row_store(v, LT_OUTF(out, val_raw) + q);
+      } else if (LT_OUTF(out, val_raw) && LT_AB_NO_YEAR_STORES < 2) {  // the other per-year planes: the year-major output loop
+        __builtin_nontemporal_store(nan, LT_OUTF(out, val_raw) + q);
       }
     }
   }
@@ -1483,17 +1484,17 @@ __device__ inline int analyze_fast(const DevScene& S_launch, const lt_params& P,
         }
       };
       if (r.uni) {
-        put(out.val_fit, r.fv);
-        put(out.fit_m, r.fm);
-        put(out.fit_b, r.fb);
-        put(out.right_m, r.rm);
-        put(out.right_b, r.rb);
+        put(LT_OUTF(out, val_fit), r.fv);
+        put(LT_OUTF(out, fit_m), r.fm);
+        put(LT_OUTF(out, fit_b), r.fb);
+        put(LT_OUTF(out, right_m), r.rm);
+        put(LT_OUTF(out, right_b), r.rb);
       } else {
-        put(out.val_fit, r.pr ? r.fv : nan);
-        put(out.fit_m, r.pr ? r.fm : nan);
-        put(out.fit_b, r.pr ? r.fb : nan);
-        put(out.right_m, r.pr ? r.rm : nan);
-        put(out.right_b, r.pr ? r.rb : nan);
+        put(LT_OUTF(out, val_fit), r.pr ? r.fv : nan);
+        put(LT_OUTF(out, fit_m), r.pr ? r.fm : nan);
+        put(LT_OUTF(out, fit_b), r.pr ? r.fb : nan);
+        put(LT_OUTF(out, right_m), r.pr ? r.rm : nan);
+        put(LT_OUTF(out, right_b), r.pr ? r.rb : nan);
       }
     };
     for (int y = 0; y < Y; y++) {    // wave-uniform
@@ -1561,8 +1562,8 @@ __device__ inline int analyze_fast(const DevScene& S_launch, const lt_params& P,
           spk |= (uint64_t)sp << y;
           vtx |= (uint64_t)isv << y;
         } else {
-          if (out.spike) out.spike[o] = sp ? 1 : 0;
-          if (out.vertex) out.vertex[o] = isv ? 1 : 0;
+          if (auto* a = LT_OUTF(out, spike)) a[o] = sp ? 1 : 0;
+          if (auto* a = LT_OUTF(out, vertex)) a[o] = isv ? 1 : 0;
         }
       }
       if (pr) {
@@ -1822,13 +1823,13 @@ __device__ inline int analyze_fast(const DevScene& S_launch, const lt_params& P,
   if (!live || deferred) {
     if (!deferred) return kDone;
     if constexpr (EXACT) {  // a binary32 resolve given a value binary32 cannot hold: unreachable
-      if (out.status) out.status[p] = status | LT_ST_NUMERIC;
+      if (auto* a = LT_OUTF(out, status)) a[p] = status | LT_ST_NUMERIC;
       return kDone;
     }
     return f32_bad ? kDeferWide : kDeferExact;
   }
-  if (out.n_years) out.n_years[p] = T;
-  if (out.status) out.status[p] = status;
+  if (auto* a = LT_OUTF(out, n_years)) a[p] = T;
+  if (auto* a = LT_OUTF(out, status)) a[p] = status;
   return kDone;
 }
 

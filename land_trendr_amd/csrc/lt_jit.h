@@ -211,7 +211,31 @@ struct Spec {
   bool masked = false, year_out = false, tl_split = false;
   lt_params params{};
   const lt::DevScene* scene = nullptr;  // the scene's tables as constants (LT_SPEC_SCENE)
+  bool fields_on = false;  // the output planes as constants (LT_SPEC_FIELDS, lt_pixel.h LT_OUTF)
+  uint32_t fields = 0;
 };
+
+// The planes a module is specialised as present: the launch's, plus winner / val_raw kept as
+// run-time pointers for the multi-rule instances. With those two planes compile-time null the
+// winner pick keeps only its branch-free store loop: c2 (one rule) 3082 vs 2848 Mpx/s, but the
+// c3 instance (four rule slots) 2157 vs 2225 (same box, profiles/r06_run9, r06_run10)
+inline uint32_t spec_fields(uint32_t launch_mask, int rmax) {
+  return launch_mask | (rmax > 1 ? (LT_FIELD_winner | LT_FIELD_val_raw) : 0u);
+}
+
+// The launch's non-null output planes as LT_FIELD_* bits (lt_pixel.h)
+inline uint32_t out_field_mask(const lt_tile_out* o) {
+  uint32_t m = 0;
+#define LT_JIT_FIELD(f) \
+  if (o->f) m |= LT_FIELD_##f;
+  LT_JIT_FIELD(status) LT_JIT_FIELD(n_years) LT_JIT_FIELD(matched) LT_JIT_FIELD(class_val)
+  LT_JIT_FIELD(onset_year) LT_JIT_FIELD(duration) LT_JIT_FIELD(magnitude)
+  LT_JIT_FIELD(initial_val) LT_JIT_FIELD(winner) LT_JIT_FIELD(val_raw) LT_JIT_FIELD(val_fit)
+  LT_JIT_FIELD(fit_m) LT_JIT_FIELD(fit_b) LT_JIT_FIELD(right_m) LT_JIT_FIELD(right_b)
+  LT_JIT_FIELD(spike) LT_JIT_FIELD(vertex)
+#undef LT_JIT_FIELD
+  return m;
+}
 
 // a DevScene as a C++ initializer (the arrays up to their used length; the rest zero-fills)
 inline std::string fmt_scene(const lt::DevScene& S) {
@@ -241,7 +265,8 @@ inline std::string fmt_rule(const lt_rule& r) {
 // compile-time switches, LT_JIT_WAVES the analyze kernel's occupancy): part of spec_key
 inline std::string env_switches() {
   std::string r;
-  for (const char* v : {"LT_JIT_DEFINES", "LT_JIT_WAVES", "LT_JIT_WPB", "LT_JIT_OVERRIDE_DIR"}) {
+  for (const char* v : {"LT_JIT_DEFINES", "LT_JIT_WAVES", "LT_JIT_WPB", "LT_JIT_OVERRIDE_DIR",
+                        "LT_JIT_FIELDS", "LT_JIT_FIELDS_OR"}) {
     const char* e = getenv(v);
     r += std::string(v) + "=" + (e ? e : "") + ";";
   }
@@ -275,8 +300,8 @@ inline uint64_t spec_key(const lt_index_prog& P, int maxy, int rmax, const char*
   }
   const int inst[3] = {maxy, rmax, (int)strlen(vt)};
   h = fnv1a_bytes(inst, sizeof inst, fnv1a(std::string(vt), h));
-  const int flags[5] = {sp.on ? 1 : 0, sp.n_years, sp.masked ? 1 : 0, sp.year_out ? 1 : 0,
-                        sp.tl_split ? 1 : 0};
+  const int flags[7] = {sp.on ? 1 : 0, sp.n_years, sp.masked ? 1 : 0, sp.year_out ? 1 : 0,
+                        sp.tl_split ? 1 : 0, sp.fields_on ? 1 : 0, (int)sp.fields};
   h = fnv1a_bytes(flags, sizeof flags, h);
   if (sp.on) {
     const lt_params& Q = sp.params;
@@ -344,6 +369,10 @@ inline std::string source(const lt_index_prog& P, int maxy, int rmax, const char
              sp.n_years, sp.masked ? 1 : 0, sp.year_out ? 1 : 0, sp.tl_split ? 1 : 0, Q.n_rules,
              Q.pre_threshold_mode, Q.line_cost);
     src += d;
+    if (sp.fields_on) {
+      snprintf(d, sizeof d, "#define LT_SPEC_FIELDS 0x%xu\n", (unsigned)sp.fields);
+      src += d;
+    }
     src += "__device__ constexpr lt_rule lt_spec_rules[" +
            std::to_string(Q.n_rules > 0 ? Q.n_rules : 1) + "] = {";
     for (int r = 0; r < (Q.n_rules > 0 ? Q.n_rules : 1); r++)

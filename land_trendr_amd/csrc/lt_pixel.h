@@ -17,6 +17,33 @@
 #include "../../include/lt_abi.h"
 #include "lt_lapack.h"
 
+// The output planes of lt_tile_out as bits (lt_jit.h out_field_mask). A JIT kernel specialised
+// for a launch's output fields (LT_SPEC_FIELDS) sees every plane the launch does not write as a
+// compile-time null (LT_OUTF): its code, and the values only it needs (RuleState1::init for an
+// unrequested initial_val), are dropped, which frees registers in the rule-heavy instances.
+#define LT_FIELD_status (1u << 0)
+#define LT_FIELD_n_years (1u << 1)
+#define LT_FIELD_matched (1u << 2)
+#define LT_FIELD_class_val (1u << 3)
+#define LT_FIELD_onset_year (1u << 4)
+#define LT_FIELD_duration (1u << 5)
+#define LT_FIELD_magnitude (1u << 6)
+#define LT_FIELD_initial_val (1u << 7)
+#define LT_FIELD_winner (1u << 8)
+#define LT_FIELD_val_raw (1u << 9)
+#define LT_FIELD_val_fit (1u << 10)
+#define LT_FIELD_fit_m (1u << 11)
+#define LT_FIELD_fit_b (1u << 12)
+#define LT_FIELD_right_m (1u << 13)
+#define LT_FIELD_right_b (1u << 14)
+#define LT_FIELD_spike (1u << 15)
+#define LT_FIELD_vertex (1u << 16)
+#ifdef LT_SPEC_FIELDS
+#define LT_OUTF(o, f) ((LT_SPEC_FIELDS & LT_FIELD_##f) ? (o).f : (decltype((o).f)) nullptr)
+#else
+#define LT_OUTF(o, f) ((o).f)
+#endif
+
 namespace lt {
 
 // Scene metadata in device memory (uploaded once per distinct scene by lt_analyze_tile).
@@ -91,12 +118,12 @@ struct RuleState1 {
   }
 
   __host__ __device__ __attribute__((always_inline)) void write(const lt_rule& R, const lt_tile_out& out, int64_t q) const {
-    if (out.matched) out.matched[q] = have ? 1 : 0;
-    if (out.class_val) out.class_val[q] = have ? R.class_val : LT_NODATA;
-    if (out.onset_year) out.onset_year[q] = on;
-    if (out.duration) out.duration[q] = du;
-    if (out.magnitude) out.magnitude[q] = mag;
-    if (out.initial_val) out.initial_val[q] = init;
+    if (auto* a = LT_OUTF(out, matched)) a[q] = have ? 1 : 0;
+    if (auto* a = LT_OUTF(out, class_val)) a[q] = have ? R.class_val : LT_NODATA;
+    if (auto* a = LT_OUTF(out, onset_year)) a[q] = on;
+    if (auto* a = LT_OUTF(out, duration)) a[q] = du;
+    if (auto* a = LT_OUTF(out, magnitude)) a[q] = mag;
+    if (auto* a = LT_OUTF(out, initial_val)) a[q] = init;
   }
 };
 

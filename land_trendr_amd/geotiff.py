@@ -99,7 +99,11 @@ class GeoTiff:
                 continue
             code, size = _TYPES[typ]
             nbytes = size * cnt
-            raw = val[:nbytes] if nbytes <= 4 else d[struct.unpack(bo + 'I', val)[0]:][:nbytes]
+            if nbytes <= 4:
+                raw = val[:nbytes]
+            else:  # (d[o:][:n] would copy the rest of the file first: 0.14 s per 174 MB raster)
+                o = struct.unpack(bo + 'I', val)[0]
+                raw = d[o:o + nbytes]
             if typ == 2:
                 tags[tag] = raw.decode('latin-1')
             elif typ in (5, 10):

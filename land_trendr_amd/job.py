@@ -232,11 +232,19 @@ class LocalJob:
         # the trendline planes: a ring of three tiles' buffers on the GPU (tile k reuses tile
         # k-3's once its rows have reached the host), so a rank's HBM never holds all its tiles'
         # trendlines
+        # LT_JOB_JIT: 'off' (default) — the precompiled kernels (a linear index_eqn fused into
+        # them, any other through the load kernel): a scene's analysis is ~1 % of a job's time
+        # (tools/job_bench.py: 49 Mpx in ~20 ms of kernels against seconds of decode and IO),
+        # while a hiprtc compile takes ~10 s of host time and, left running on its worker thread
+        # past the analysis, slowed the output step 13x (profiles/r06_run6d); 'async' — the module
+        # compiles on a worker thread while the first tiles run precompiled (same results);
+        # 'sync' — compile first (a disk-cached module loads at once)
+        jit_mode = os.environ.get('LT_JOB_JIT', 'sync' if os.environ.get('LT_JOB_JIT_SYNC') == '1'
+                                  else 'off')
         runner = MosaicRunner(eng, m, params, items, label_fields + tl_fields, fn, dist,
-                              exchange_fields=label_fields, ring=3 if cuda else 0)
-        # the JIT module compiles on a worker thread while the first tiles run on the precompiled
-        # kernels (same results): a job never stalls ~10 s for hiprtc (LT_JOB_JIT_SYNC=1: waits)
-        jit_async = cuda and runner.jit is not None and os.environ.get('LT_JOB_JIT_SYNC') != '1'
+                              exchange_fields=label_fields, ring=3 if cuda else 0,
+                              jit=jit_mode != 'off')
+        jit_async = cuda and runner.jit is not None and jit_mode == 'async'
         if jit_async:
             eng.set_jit_mode(True)
             runner.prepare_jit(wait=False)

@@ -51,11 +51,13 @@ class MosaicRunner:
     ring: 0, every tile has planes of its own for the fields not exchanged (the trendline
     planes); R > 0, tile k writes them into buffer k % R of a ring (one tile per call), and
     step()'s slab_free(j) names the event after which tile j's buffer may be overwritten (its
-    D2H copies done): the rank's HBM then holds R tiles' trendline planes, not all of them."""
+    D2H copies done): the rank's HBM then holds R tiles' trendline planes, not all of them.
+    jit: False keeps the index_eqn program off the JIT kernels (a linear program then runs in
+    the precompiled kernels, any other through the load kernel), as LT_JIT_INDEX=0 does."""
 
     def __init__(self, engine, mosaic, params, items, fields, index_fn=None, dist=None,
                  exchange_fields=LABEL_GATHER_FIELDS, load_stream=True, group=0, dst=0,
-                 fused=None, ring=0):
+                 fused=None, ring=0, jit=True):
         self.eng, self.m, self.params, self.items = engine, mosaic, params, list(items)
         self.fields = tuple(fields)
         self.index_fn = index_fn
@@ -106,7 +108,7 @@ class MosaicRunner:
         if fused is None:
             fused = os.environ.get('LT_FUSED_INDEX', '1') != '0'
         all_bands = has_bands and all(it.bands is not None for it in self.items)
-        jit_ok = (fused and all_bands and self.cuda and
+        jit_ok = (fused and all_bands and self.cuda and jit and
                   os.environ.get('LT_JIT_INDEX', '1') != '0')
         self.lin = getattr(index_fn, 'lin', None) if fused and all_bands else None
         # a linear program too goes to the JIT kernels, specialised for the job's configuration

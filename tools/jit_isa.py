@@ -18,7 +18,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def jit_source(cfg_name, pixels=64, flags=3):
+def jit_source(cfg_name, pixels=64, flags=None):
+    """flags None: bench.py's launch (spec + scene + its output fields)."""
     import bench
     from land_trendr_amd import _abi
     from land_trendr_amd.index_eqn import IndexProgram
@@ -32,6 +33,15 @@ def jit_source(cfg_name, pixels=64, flags=3):
     params, _ = compile_params(c['line_cost'], c['rules'], c['mode'])
     prog = IndexProgram('B1 - B2', band_dtype='int16').to_c()
     lib = _abi.load_lib()
+    if flags is None:
+        fields = ['status', 'matched', 'class_val', 'onset_year', 'duration', 'magnitude']
+        if c['trendline']:
+            fields += bench.TRENDLINE_FIELDS
+        mask = 0
+        for f in fields:
+            mask |= _abi.LT_FIELD_BITS[f]
+        flags = (_abi.LT_JIT_SRC_SPEC | _abi.LT_JIT_SRC_SCENE | _abi.LT_JIT_SRC_FIELDS |
+                 (mask << 8))
     scn = meta.to_c()
     args = (ctypes.byref(scn), ctypes.byref(params), ctypes.byref(prog),
             1 if c['mask'] > 0 else 0, 1 if c['trendline'] else 0, flags)
