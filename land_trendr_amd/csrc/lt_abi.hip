@@ -592,6 +592,7 @@ static int jit_acquire(lt_ctx* c, const lt_index* f, int Y, const lt_params* prm
         getenv("LT_JIT_FIELDS_OR") ? (uint32_t)strtoul(getenv("LT_JIT_FIELDS_OR"), nullptr, 16) : 0u;
     sp.fields_on = fields_on;
     sp.fields = fields_on ? lt_jit::spec_fields(lt_jit::out_field_mask(o) | fields_or, rmax) : 0u;
+    sp.vbits = in->obs_valid_bits != nullptr && scene->n_obs <= 128;
   }
   uint64_t key = lt_jit::spec_key(f->prog, maxy, rmax, vt, sp);
   auto it = c->jit.find(key);
@@ -1220,6 +1221,7 @@ int lt_jit_source(const lt_scene* sc, const lt_params* prm, const lt_index_prog*
     if (flags & LT_JIT_SRC_FIELDS) {  // the output-field mask in bits 8.. of flags
       sp.fields_on = true;
       sp.fields = lt_jit::spec_fields((uint32_t)flags >> 8, rmax);
+      sp.vbits = masked != 0 && tmp.n_obs <= 128;  // the bit planes bench.py and the job pass
     }
   }
   std::string err;

@@ -267,7 +267,12 @@ __device__ inline int analyze_fast(const DevScene& S_launch, const lt_params& P,
   // per observation, each waited out before its year's comparison
 #ifdef LT_SPEC_MASKED
   constexpr bool masked = LT_SPEC_MASKED != 0;
+#ifdef LT_SPEC_VBITS
+  // the mask's format as a constant (lt_jit.h Spec::vbits): one of the two scans is compiled
+  constexpr bool vbits = masked && LT_SPEC_VBITS != 0;
+#else
   const bool vbits = masked && in.obs_valid_bits != nullptr && S.n_obs <= 128;
+#endif
 #else
   const bool masked = in.obs_valid != nullptr || in.obs_valid_bits != nullptr;  // launch-uniform
   const bool vbits = in.obs_valid_bits != nullptr && S.n_obs <= 128;

@@ -213,6 +213,9 @@ struct Spec {
   const lt::DevScene* scene = nullptr;  // the scene's tables as constants (LT_SPEC_SCENE)
   bool fields_on = false;  // the output planes as constants (LT_SPEC_FIELDS, lt_pixel.h LT_OUTF)
   uint32_t fields = 0;
+  // with fields_on: the cloud mask comes as bit planes (obs_valid_bits, <= 128 observations) —
+  // LT_SPEC_VBITS 1 — or as bytes (0)
+  bool vbits = false;
 };
 
 // The planes a module is specialised as present: the launch's, plus winner / val_raw kept as
@@ -300,8 +303,9 @@ inline uint64_t spec_key(const lt_index_prog& P, int maxy, int rmax, const char*
   }
   const int inst[3] = {maxy, rmax, (int)strlen(vt)};
   h = fnv1a_bytes(inst, sizeof inst, fnv1a(std::string(vt), h));
-  const int flags[7] = {sp.on ? 1 : 0, sp.n_years, sp.masked ? 1 : 0, sp.year_out ? 1 : 0,
-                        sp.tl_split ? 1 : 0, sp.fields_on ? 1 : 0, (int)sp.fields};
+  const int flags[8] = {sp.on ? 1 : 0, sp.n_years, sp.masked ? 1 : 0, sp.year_out ? 1 : 0,
+                        sp.tl_split ? 1 : 0, sp.fields_on ? 1 : 0, (int)sp.fields,
+                        sp.vbits ? 1 : 0};
   h = fnv1a_bytes(flags, sizeof flags, h);
   if (sp.on) {
     const lt_params& Q = sp.params;
@@ -370,7 +374,8 @@ inline std::string source(const lt_index_prog& P, int maxy, int rmax, const char
              Q.pre_threshold_mode, Q.line_cost);
     src += d;
     if (sp.fields_on) {
-      snprintf(d, sizeof d, "#define LT_SPEC_FIELDS 0x%xu\n", (unsigned)sp.fields);
+      snprintf(d, sizeof d, "#define LT_SPEC_FIELDS 0x%xu\n#define LT_SPEC_VBITS %d\n",
+               (unsigned)sp.fields, sp.vbits ? 1 : 0);
       src += d;
     }
     src += "__device__ constexpr lt_rule lt_spec_rules[" +
