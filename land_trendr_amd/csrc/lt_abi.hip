@@ -593,6 +593,10 @@ static int jit_acquire(lt_ctx* c, const lt_index* f, int Y, const lt_params* prm
     sp.fields_on = fields_on;
     sp.fields = fields_on ? lt_jit::spec_fields(lt_jit::out_field_mask(o) | fields_or, rmax) : 0u;
     sp.vbits = in->obs_valid_bits != nullptr && scene->n_obs <= 128;
+    sp.band_pair = f->prog.n_bands == 2 &&
+                   (f->prog.band_type == LT_T_I16 || f->prog.band_type == LT_T_U16) &&
+                   in->band_stride == 1 && in->band_pix_stride == 2 &&
+                   in->band_obs_stride % 2 == 0 && ((uintptr_t)in->obs_bands & 3) == 0;
   }
   uint64_t key = lt_jit::spec_key(f->prog, maxy, rmax, vt, sp);
   auto it = c->jit.find(key);
@@ -1222,6 +1226,9 @@ int lt_jit_source(const lt_scene* sc, const lt_params* prm, const lt_index_prog*
       sp.fields_on = true;
       sp.fields = lt_jit::spec_fields((uint32_t)flags >> 8, rmax);
       sp.vbits = masked != 0 && tmp.n_obs <= 128;  // the bit planes bench.py and the job pass
+      // bench.py's pixel-interleaved int16 pair
+      sp.band_pair = prog->n_bands == 2 &&
+                     (prog->band_type == LT_T_I16 || prog->band_type == LT_T_U16);
     }
   }
   std::string err;

@@ -421,6 +421,26 @@ __device__ inline int analyze_fast(const DevScene& S_launch, const lt_params& P,
     // a JIT kernel (lt_jit.h): the tile's index_eqn program is inlined as lt_jit_index (the load
     // kernel's straight-line code and store, lt_index.h codegen), evaluated on every winner's
     // band values, all the batch's band loads issued first
+#if defined(LT_SPEC_BAND_PAIR) && LT_SPEC_BAND_PAIR
+    {
+      // two 16-bit bands pixel-interleaved, 4-byte aligned (lt_jit.h Spec::band_pair): a pixel's
+      // pair is one 32-bit load, nontemporal (read once; the x-set table stays L2-hot), band 0 in
+      // the low half, as the fused linear path reads it (fused16)
+      const int32_t* bw = (const int32_t*)in.obs_bands;
+      const int64_t os2 = in.band_obs_stride >> 1;
+      int32_t w[WB];
+#pragma unroll
+      for (int u = 0; u < WB; u++)
+        w[u] = __builtin_nontemporal_load(
+            &(bw + (uni ? row_of(u, Uni{}) : row_of(u, Lane{})) * os2)[pp]);
+#pragma unroll
+      for (int u = 0; u < WB; u++) {
+        const LT_JIT_BAND_T b2[2] = {(LT_JIT_BAND_T)(w[u] & 0xffff),
+                                     (LT_JIT_BAND_T)((uint32_t)w[u] >> 16)};
+        val[u] = lt_jit_index(b2, 1);
+      }
+    }
+#else
     {
       const LT_JIT_BAND_T* bb = (const LT_JIT_BAND_T*)in.obs_bands;
       const LT_JIT_BAND_T* at[WB];
@@ -431,6 +451,7 @@ __device__ inline int analyze_fast(const DevScene& S_launch, const lt_params& P,
 #pragma unroll
       for (int u = 0; u < WB; u++) val[u] = lt_jit_index(at[u], in.band_stride);
     }
+#endif
 #else
     if (in.obs_bands) {
       const lt_index_lin& LN = in.lin;

@@ -216,6 +216,9 @@ struct Spec {
   // with fields_on: the cloud mask comes as bit planes (obs_valid_bits, <= 128 observations) —
   // LT_SPEC_VBITS 1 — or as bytes (0)
   bool vbits = false;
+  // with fields_on: two 16-bit bands pixel-interleaved (band_stride 1, band_pix_stride 2), the
+  // tile 4-byte aligned with an even obs stride: one 32-bit load per winner (LT_SPEC_BAND_PAIR)
+  bool band_pair = false;
 };
 
 // The planes a module is specialised as present: the launch's, plus winner / val_raw kept as
@@ -305,7 +308,7 @@ inline uint64_t spec_key(const lt_index_prog& P, int maxy, int rmax, const char*
   h = fnv1a_bytes(inst, sizeof inst, fnv1a(std::string(vt), h));
   const int flags[8] = {sp.on ? 1 : 0, sp.n_years, sp.masked ? 1 : 0, sp.year_out ? 1 : 0,
                         sp.tl_split ? 1 : 0, sp.fields_on ? 1 : 0, (int)sp.fields,
-                        sp.vbits ? 1 : 0};
+                        (sp.vbits ? 1 : 0) | (sp.band_pair ? 2 : 0)};
   h = fnv1a_bytes(flags, sizeof flags, h);
   if (sp.on) {
     const lt_params& Q = sp.params;
@@ -374,8 +377,9 @@ inline std::string source(const lt_index_prog& P, int maxy, int rmax, const char
              Q.pre_threshold_mode, Q.line_cost);
     src += d;
     if (sp.fields_on) {
-      snprintf(d, sizeof d, "#define LT_SPEC_FIELDS 0x%xu\n#define LT_SPEC_VBITS %d\n",
-               (unsigned)sp.fields, sp.vbits ? 1 : 0);
+      snprintf(d, sizeof d,
+               "#define LT_SPEC_FIELDS 0x%xu\n#define LT_SPEC_VBITS %d\n#define LT_SPEC_BAND_PAIR %d\n",
+               (unsigned)sp.fields, sp.vbits ? 1 : 0, sp.band_pair ? 1 : 0);
       src += d;
     }
     src += "__device__ constexpr lt_rule lt_spec_rules[" +
