@@ -121,7 +121,7 @@ def pmc_summary(config, build):
     newest, whose '_matches_build' is then False and whose counters describe another build."""
     name = {'c4': 'c2'}.get(config, config)
     found = []
-    for rnd in ('r05', 'r04', 'r03', 'r02'):  # newest first
+    for rnd in ('r06', 'r05', 'r04', 'r03', 'r02'):  # newest first
         path = os.path.join(ROOT, 'profiles', '%s_pmc_%s.json' % (rnd, name))
         try:
             with open(path) as f:
