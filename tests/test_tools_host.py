@@ -22,3 +22,39 @@ def test_defer_diag_classifies_the_deferred_columns():
     kinds = d['ambiguous_columns_on_deferred_paths']
     assert sum(kinds.values()) == st.get('exact_tie_columns', 0) + st.get('near_tie_columns', 0)
     assert sum(kinds.values()) >= st['deferred']
+
+
+def test_dp_lockstep_model_counts_starts_per_column():
+    """tools/dp_lockstep_model.py (DESIGN.md § The DP's lockstep cost): the wave prices at least
+    the lanes' mean, and a budget of one start per column defers most pixels."""
+    out = subprocess.check_output([sys.executable, os.path.join(ROOT, 'tools',
+                                                                'dp_lockstep_model.py'),
+                                   '--config', 'c2', '--pixels', '640'], cwd=ROOT, timeout=300)
+    d = json.loads(out)
+    assert d['pixels'] == 640 and d['columns'] > 0
+    assert d['wave_starts_per_column'] >= d['lane_mean_starts_per_column'] > 0.5
+    assert d['budget']['1']['deferred_frac'] > d['budget']['3']['deferred_frac']
+
+
+def test_co_patch_rewrites_only_the_resource_fields(tmp_path):
+    """tools/co_patch.py (DESIGN.md § Wrong-result variants, round 6) on a small gfx950 code
+    object: the private segment size and the VGPR allocation change in the metadata and the kernel
+    descriptor; the instructions do not."""
+    sys.path.insert(0, os.path.join(ROOT, 'tools'))
+    import jit_isa  # hiprtc, as the JIT modules are built
+    src = ('extern "C" __global__ void k(int* a, int n) {\n'
+           '  int t[40];\n'
+           '  for (int i = 0; i < 40; i++) t[(i * 7 + threadIdx.x) % 40] = i + n;\n'
+           '  a[threadIdx.x] = t[(threadIdx.x + n) % 40];\n}\n')
+    co = str(tmp_path / 'k.co')
+    with open(co, 'wb') as f:
+        f.write(jit_isa.hiprtc_compile(src))
+    out = str(tmp_path / 'p.co')
+    subprocess.check_call([sys.executable, os.path.join(ROOT, 'tools', 'co_patch.py'), co, out,
+                           '--private', '248', '--vgprs', '120'], timeout=60)
+    ro = '/opt/rocm/lib/llvm/bin/llvm-readelf'
+    notes = subprocess.check_output([ro, '--notes', out]).decode()
+    assert '.private_segment_fixed_size: 248' in notes and '.vgpr_count:     120' in notes
+    dis = [subprocess.check_output(['/opt/rocm/lib/llvm/bin/llvm-objdump', '-d', '--mcpu=gfx950',
+                                    f]).decode().split('\n', 3)[3] for f in (co, out)]
+    assert dis[0] == dis[1]

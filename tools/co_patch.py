@@ -97,8 +97,11 @@ def patch(src, dst, private, kernels=None, vgprs=None):
             if data[v] == 0xcd:  # uint16
                 old = struct.unpack('>H', data[v + 1:v + 3])[0]
                 data[v + 1:v + 3] = struct.pack('>H', private)
-            elif data[v] == 0xcc:
-                raise SystemExit('1-byte msgpack size: re-encode needed')
+            elif data[v] == 0xcc:  # uint8: only a value that still fits
+                old = data[v + 1]
+                if private > 255:
+                    raise SystemExit('uint8 size %d: cannot widen in place' % old)
+                data[v + 1] = private
             else:  # positive fixint: only when the new value also fits
                 old = data[v]
                 if private > 127:
