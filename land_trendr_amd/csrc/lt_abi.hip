@@ -597,6 +597,8 @@ static int jit_acquire(lt_ctx* c, const lt_index* f, int Y, const lt_params* prm
                    (f->prog.band_type == LT_T_I16 || f->prog.band_type == LT_T_U16) &&
                    in->band_stride == 1 && in->band_pix_stride == 2 &&
                    in->band_obs_stride % 2 == 0 && ((uintptr_t)in->obs_bands & 3) == 0;
+    static const bool full_on = !(getenv("LT_JIT_FULL") && getenv("LT_JIT_FULL")[0] == '0');
+    sp.full = full_on && in->n_pix % (64 * lt_jit::analyze_wpb()) == 0;
   }
   uint64_t key = lt_jit::spec_key(f->prog, maxy, rmax, vt, sp);
   auto it = c->jit.find(key);
@@ -1229,6 +1231,7 @@ int lt_jit_source(const lt_scene* sc, const lt_params* prm, const lt_index_prog*
       // bench.py's pixel-interleaved int16 pair
       sp.band_pair = prog->n_bands == 2 &&
                      (prog->band_type == LT_T_I16 || prog->band_type == LT_T_U16);
+      sp.full = true;  // bench.py's tiles are whole waves
     }
   }
   std::string err;

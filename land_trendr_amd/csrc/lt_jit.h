@@ -219,6 +219,9 @@ struct Spec {
   // with fields_on: two 16-bit bands pixel-interleaved (band_stride 1, band_pix_stride 2), the
   // tile 4-byte aligned with an even obs stride: one 32-bit load per winner (LT_SPEC_BAND_PAIR)
   bool band_pair = false;
+  // with fields_on: the tile is a whole number of the analyze kernel's workgroups (every lane of
+  // every wave has a pixel: LT_SPEC_FULL)
+  bool full = false;
 };
 
 // The planes a module is specialised as present: the launch's, plus winner / val_raw kept as
@@ -272,7 +275,7 @@ inline std::string fmt_rule(const lt_rule& r) {
 inline std::string env_switches() {
   std::string r;
   for (const char* v : {"LT_JIT_DEFINES", "LT_JIT_WAVES", "LT_JIT_WPB", "LT_JIT_OVERRIDE_DIR",
-                        "LT_JIT_FIELDS", "LT_JIT_FIELDS_OR"}) {
+                        "LT_JIT_FIELDS", "LT_JIT_FIELDS_OR", "LT_JIT_FULL"}) {
     const char* e = getenv(v);
     r += std::string(v) + "=" + (e ? e : "") + ";";
   }
@@ -308,7 +311,7 @@ inline uint64_t spec_key(const lt_index_prog& P, int maxy, int rmax, const char*
   h = fnv1a_bytes(inst, sizeof inst, fnv1a(std::string(vt), h));
   const int flags[8] = {sp.on ? 1 : 0, sp.n_years, sp.masked ? 1 : 0, sp.year_out ? 1 : 0,
                         sp.tl_split ? 1 : 0, sp.fields_on ? 1 : 0, (int)sp.fields,
-                        (sp.vbits ? 1 : 0) | (sp.band_pair ? 2 : 0)};
+                        (sp.vbits ? 1 : 0) | (sp.band_pair ? 2 : 0) | (sp.full ? 4 : 0)};
   h = fnv1a_bytes(flags, sizeof flags, h);
   if (sp.on) {
     const lt_params& Q = sp.params;
@@ -378,8 +381,9 @@ inline std::string source(const lt_index_prog& P, int maxy, int rmax, const char
     src += d;
     if (sp.fields_on) {
       snprintf(d, sizeof d,
-               "#define LT_SPEC_FIELDS 0x%xu\n#define LT_SPEC_VBITS %d\n#define LT_SPEC_BAND_PAIR %d\n",
-               (unsigned)sp.fields, sp.vbits ? 1 : 0, sp.band_pair ? 1 : 0);
+               "#define LT_SPEC_FIELDS 0x%xu\n#define LT_SPEC_VBITS %d\n#define LT_SPEC_BAND_PAIR %d\n"
+               "#define LT_SPEC_FULL %d\n",
+               (unsigned)sp.fields, sp.vbits ? 1 : 0, sp.band_pair ? 1 : 0, sp.full ? 1 : 0);
       src += d;
     }
     src += "__device__ constexpr lt_rule lt_spec_rules[" +

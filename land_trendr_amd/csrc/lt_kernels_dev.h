@@ -84,7 +84,13 @@ __device__ inline void analyze_body() {
 #endif
   const int64_t p = xcd_block(blockIdx.x, gridDim.x) * (64 * LT_WPB) + threadIdx.x;
   const int64_t n_pix = K.in.n_pix;
+#if defined(LT_SPEC_FULL) && LT_SPEC_FULL
+  // the tile is whole waves (lt_jit.h Spec::full): every lane has a pixel
+  const bool live = true;
+  (void)n_pix;
+#else
   const bool live = p < n_pix;
+#endif
   const int d = analyze_fast<MAXY, RMAX, false, VT>(*K.S, K.P, K.in, K.out, K.xtab, K.yflags,
                                                     K.tl_bits, K.tl_eqn, p, live, lane, L,
                                                     Probe{});
