@@ -58,3 +58,35 @@ def test_co_patch_rewrites_only_the_resource_fields(tmp_path):
     dis = [subprocess.check_output(['/opt/rocm/lib/llvm/bin/llvm-objdump', '-d', '--mcpu=gfx950',
                                     f]).decode().split('\n', 3)[3] for f in (co, out)]
     assert dis[0] == dis[1]
+
+
+def test_co_patch_waitcnt_only_tightens_waits(tmp_path):
+    """co_patch.py --waitcnt: every s_waitcnt of the kernel gets the chosen counter at 0, in
+    place; every other instruction and every address stays as it was."""
+    sys.path.insert(0, os.path.join(ROOT, 'tools'))
+    import jit_isa
+    src = ('extern "C" __global__ void k(const double* a, double* b, int n) {\n'
+           '  __shared__ double s[64];\n'
+           '  s[threadIdx.x] = a[threadIdx.x] * a[threadIdx.x + n];\n'
+           '  __syncthreads();\n'
+           '  b[threadIdx.x] = s[(threadIdx.x + n) & 63] + a[threadIdx.x + 2 * n];\n}\n')
+    co = str(tmp_path / 'k.co')
+    with open(co, 'wb') as f:
+        f.write(jit_isa.hiprtc_compile(src))
+    od = '/opt/rocm/lib/llvm/bin/llvm-objdump'
+    for kind, pat in (('lgkm', 'lgkmcnt(0)'), ('vm', 'vmcnt(0)')):
+        out = str(tmp_path / ('%s.co' % kind))
+        subprocess.check_call([sys.executable, os.path.join(ROOT, 'tools', 'co_patch.py'), co,
+                               out, '--waitcnt', kind], timeout=60)
+        d0, d1 = [subprocess.check_output([od, '-d', '--mcpu=gfx950', f]).decode()
+                  .split('\n', 3)[3].splitlines() for f in (co, out)]
+        assert len(d0) == len(d1)
+        n_wait = 0
+        for x, y in zip(d0, d1):
+            if 's_waitcnt' in x:
+                n_wait += 1
+                assert pat in y, y
+                assert x.split('//')[1].split(':')[0] == y.split('//')[1].split(':')[0]
+            else:
+                assert x == y
+        assert n_wait > 0

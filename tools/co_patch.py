@@ -15,8 +15,20 @@ code and a larger slot, an access beyond the declared size is the cause.
 --vgprs rewrites COMPUTE_PGM_RSRC1's granulated VGPR count (kd byte 48, bits 5:0, granules of 8
 on gfx950) and the metadata's .vgpr_count: the same code then gets more registers than it uses,
 so fewer waves share a SIMD (a lower occupancy with the LDS, scratch and code unchanged).
+
+    python tools/co_patch.py IN.co OUT.co --waitcnt lgkm [--range 0x3b00:0x9000] [--kernel K]
+
+--waitcnt makes waits stricter in place, each instruction keeping its address: every `s_waitcnt`
+(SOPP, one 32-bit word on gfx950) gets its lgkmcnt field (LDS, scalar memory, messages: bits
+11:8), its vmcnt field (vector memory: bits 3:0 and 15:14) or both set to 0, so the wave waits
+there for every outstanding access of that kind. A stricter wait can only make the code slower,
+never change what it computes: if a wrong-result variant becomes correct with every lgkm wait at
+zero and identical code otherwise, a wait that let an LDS or scalar-memory result be used before
+it arrived (or a hazard those accesses hide) is the cause; --range (virtual addresses, hex) and
+--kernel narrow it down by bisection.
 """
 import argparse
+import re
 import struct
 import subprocess
 
@@ -81,8 +93,61 @@ def patch_vgprs(data, names, vgprs, kernels, kds):
             data[off + 48:off + 52] = struct.pack('<I', r1)
 
 
-def patch(src, dst, private, kernels=None, vgprs=None):
+OBJDUMP = '/opt/rocm/lib/llvm/bin/llvm-objdump'
+WAIT_CLEAR = {'lgkm': 0x0F00, 'vm': 0xC00F, 'all': 0xCF0F}
+
+
+def func_ranges(path):
+    """{kernel name: (start, end)} virtual address ranges of the FUNC symbols."""
+    out = subprocess.check_output([READELF, '-s', '--wide', path]).decode()
+    res = {}
+    for ln in out.splitlines():
+        f = ln.split()
+        if len(f) == 8 and f[3] == 'FUNC':
+            a = int(f[1], 16)
+            res[f[7]] = (a, a + int(f[2]))
+    return res
+
+
+def text_section(path):
+    """(address, file offset, size) of .text."""
+    out = subprocess.check_output([READELF, '-S', '--wide', path]).decode()
+    for ln in out.splitlines():
+        if '] .text ' in ln:
+            g = ln.split(']')[1].split()
+            return int(g[2], 16), int(g[3], 16), int(g[4], 16)
+    raise SystemExit('no .text in %s' % path)
+
+
+def patch_waitcnt(data, path, kind, lo=None, hi=None, kernels=None):
+    """Zero the `kind` counter fields of every s_waitcnt in [lo, hi) (and in `kernels`); returns
+    (waits seen in range, waits changed)."""
+    addr0, off0, size = text_section(path)
+    fr = func_ranges(path)
+    asm = subprocess.check_output([OBJDUMP, '-d', '--mcpu=gfx950', path]).decode()
+    seen = changed = 0
+    for m in re.finditer(r'\ts_waitcnt [^\n]*// ([0-9A-F]+): ([0-9A-F]{8})\n', asm):
+        a, word = int(m.group(1), 16), int(m.group(2), 16)
+        if (lo is not None and a < lo) or (hi is not None and a >= hi):
+            continue
+        if kernels is not None and not any(fr[k][0] <= a < fr[k][1] for k in kernels):
+            continue
+        assert addr0 <= a < addr0 + size and word >> 16 == 0xBF8C, (hex(a), hex(word))
+        o = a - addr0 + off0
+        assert struct.unpack('<I', data[o:o + 4])[0] == word, hex(a)
+        new = word & ~WAIT_CLEAR[kind]
+        seen += 1
+        if new != word:
+            data[o:o + 4] = struct.pack('<I', new)
+            changed += 1
+    return seen, changed
+
+
+def patch(src, dst, private, kernels=None, vgprs=None, waitcnt=None, rng=(None, None)):
     data = bytearray(open(src, 'rb').read())
+    if waitcnt is not None:
+        seen, changed = patch_waitcnt(data, src, waitcnt, rng[0], rng[1], kernels)
+        print('s_waitcnt: %d in range, %d made stricter (%s -> 0)' % (seen, changed, waitcnt))
     names = kernel_meta_ranges(bytes(data))
     done = []
     if vgprs is not None:
@@ -123,8 +188,16 @@ def main():
     ap.add_argument('--private', type=int, default=None, help='bytes per lane')
     ap.add_argument('--vgprs', type=int, default=None, help='VGPRs per lane (multiple of 8)')
     ap.add_argument('--kernel', action='append', default=None)
+    ap.add_argument('--waitcnt', choices=sorted(WAIT_CLEAR), default=None,
+                    help='set this counter of every s_waitcnt to 0 (stricter waits, same code)')
+    ap.add_argument('--range', default=None, help='LO:HI virtual addresses (hex) for --waitcnt')
     a = ap.parse_args()
-    done = patch(a.src, a.dst, a.private, set(a.kernel) if a.kernel else None, a.vgprs)
+    rng = (None, None)
+    if a.range:
+        lo, hi = a.range.split(':')
+        rng = (int(lo, 16) if lo else None, int(hi, 16) if hi else None)
+    done = patch(a.src, a.dst, a.private, set(a.kernel) if a.kernel else None, a.vgprs,
+                 a.waitcnt, rng)
     print('patched %s -> %s: private %s (%s), vgprs %s'
           % (a.src, a.dst, a.private, ', '.join('%s was %d' % d for d in done), a.vgprs))
 

@@ -131,6 +131,9 @@ def main():
         waves = sorted({p // 64 for p in bad_px})
         wpix = [p for w in waves for p in range(w * 64, min(P, w * 64 + 64))]
         res['in_their_waves_mismatching'] = rerun(wpix)
+    # which code ran: disk_hits counts the LT_JIT_OVERRIDE_DIR code objects loaded (or cached)
+    res['jit'] = {k: v for k, v in eng.jit_stats().items() if k != 'last_error'}
+    res['jit_override_dir'] = os.environ.get('LT_JIT_OVERRIDE_DIR')
     print(json.dumps(res), flush=True)
 
 
