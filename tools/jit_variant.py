@@ -66,11 +66,21 @@ def main():
                     help='a tree holding modified copies of the kernel headers (same layout): the '
                          'override is built from them, the library and its build hash stay as '
                          'they are')
+    ap.add_argument('--sub', action='append', default=[],
+                    help='OLD=>NEW: a text substitution in the generated source before compiling '
+                         '(e.g. another __launch_bounds__); the override keeps the name of the '
+                         'unmodified source, so the runtime loads it in its place')
     a = ap.parse_args()
     if a.define:
         os.environ['LT_JIT_DEFINES'] = ','.join(a.define)
     src = jit_isa.jit_source(a.config)
-    code = compile_rtc(src, a.opt, hdr_root=a.hdr_root)
+    csrc = src
+    for sub in a.sub:
+        old, new = sub.split('=>')
+        if old not in csrc:
+            raise SystemExit('--sub: %r not in the generated source' % old)
+        csrc = csrc.replace(old, new)
+    code = compile_rtc(csrc, a.opt, hdr_root=a.hdr_root)
     os.makedirs(a.out, exist_ok=True)
     name = os.path.join(a.out, 'lt_src_%016x.co' % jit_asm.fnv1a(src.encode()))
     with open(name, 'wb') as fh:
