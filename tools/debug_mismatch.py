@@ -53,7 +53,23 @@ def main():
     ap.add_argument('--sample', type=int, default=200000)
     ap.add_argument('--pixels', type=int, default=0)
     ap.add_argument('--no-rerun', action='store_true', help='skip the isolation reruns')
+    ap.add_argument('--poison', default=None,
+                    help='HEX[,HEX]: before step 1 (and 2) fill every SIMD\'s register file with '
+                         'this 32-bit pattern (build/bin/libreg_poison.so, tools/reg_poison.hip)')
     a = ap.parse_args()
+    pois = None
+    if a.poison:
+        import ctypes
+        pl = ctypes.CDLL(os.path.join(ROOT, 'build', 'bin', 'libreg_poison.so'))
+        pl.lt_reg_poison.argtypes = [ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p]
+        pats = [int(x, 16) for x in a.poison.split(',')]
+        pats = pats + pats[-1:] * (2 - len(pats))
+
+        def pois(k):  # one wave per SIMD: 4 waves per CU x 256 CUs, 4x over
+            torch.cuda.synchronize()
+            rc = pl.lt_reg_poison(pats[k], 4096, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+            torch.cuda.synchronize()
+            assert rc == 0, rc
     c = bench.CONFIGS[a.config]
     P = a.pixels or c['pixels']
     eng = get_engine(0)
@@ -64,11 +80,15 @@ def main():
     params, _ = compile_params(c['line_cost'], c['rules'], c['mode'])
     fn = eng.compile_index(IndexProgram('B1 - B2', band_dtype='int16'))
     r = MosaicRunner(eng, m, params, items, FIELDS, fn)
+    if pois:
+        pois(0)
     r.step()
     torch.cuda.synchronize()
     print('step 1 done', file=sys.stderr, flush=True)
     first = {f: r.outs[0][f].clone() for f in FIELDS}
     # determinism: the same launch again, every output plane compared bitwise with the first
+    if pois:
+        pois(1)
     r.step()
     torch.cuda.synchronize()
     print('step 2 done', file=sys.stderr, flush=True)
@@ -134,6 +154,7 @@ def main():
     # which code ran: disk_hits counts the LT_JIT_OVERRIDE_DIR code objects loaded (or cached)
     res['jit'] = {k: v for k, v in eng.jit_stats().items() if k != 'last_error'}
     res['jit_override_dir'] = os.environ.get('LT_JIT_OVERRIDE_DIR')
+    res['poison'] = a.poison
     print(json.dumps(res), flush=True)
 
 
