@@ -4,10 +4,11 @@
 #      trace of the same default command
 #   P  PMC passes (profiles/pmc_passes.sh, build stamped) of the launches bench.py times: c2 and c3
 #      one 49 Mpx launch each, c5 its 16.8 Mpx tiles of the 49 Mpx scene
-#   B  c3 / c4 / c5 bench lines; whole-scene parity of bench's exact c2 and c3 launches (every pixel
-#      against the oracle); run-to-run determinism of the same launches (tools/debug_mismatch.py)
+#   B  c3 / c4 / c5 bench lines; run-to-run determinism of bench's exact c2 and c3 launches
+#      (tools/debug_mismatch.py)
+#   F  whole-scene parity of bench's exact c2 and c3 launches (every pixel against the oracle)
 #   C  c5 whole-scene parity, all 15 fields, in two halves
-# Usage: bash profiles/r06_final.sh <outdir under gpurun_out> A|P|B|C
+# Usage: bash profiles/r06_final.sh <outdir under gpurun_out> A|P|B|F|C
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/$1
@@ -43,10 +44,14 @@ for C in c3 c4 c5; do
   python -c "import json;d=json.load(open('$O/${C}_bench.json'));r=d['roofline'];print('$C',d['value'],d['ms_per_step'],r['frac'],r['pmc_matches_build'],d['parity_sample']['mismatched_values'])"
 done
 for C in c2 c3; do
-  timeout -k 10 560 python -u tests/full_scene_check.py --config $C --labels-only --whole --bench-fields --out $O/r06_full_scene_parity_${C}_whole.json > $O/full_$C.log 2>&1
-  tail -1 $O/full_$C.log
   timeout -k 10 200 python tools/debug_mismatch.py --config $C --sample 200000 --no-rerun > $O/determinism_$C.json 2> $O/determinism_$C.err
   python -c "import json;d=json.load(open('$O/determinism_$C.json'));print('$C',{k:v for k,v in d.items() if k not in ('examples','diff_hist64','diff_first','diff_lane_hist')})"
+done
+fi
+if [ "$2" = F ]; then
+for C in c2 c3; do
+  timeout -k 10 560 python -u tests/full_scene_check.py --config $C --labels-only --whole --bench-fields --out $O/r06_full_scene_parity_${C}_whole.json > $O/full_$C.log 2>&1
+  tail -1 $O/full_$C.log
 done
 fi
 if [ "$2" = C ]; then
