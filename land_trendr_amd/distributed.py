@@ -149,6 +149,16 @@ class LabelExchange:
     def slab(self, tile):
         return self._slabs[tile.t]
 
+    def rebind(self, full):
+        """World 1 only (nothing is sent): the writer's rasters become `full` (a dict like
+        self.full), its slabs views of them. A one-tile runner's pipelined steps alternate two
+        such sets (runner._flip_bank), so a step's analyze never waits for the previous step's
+        resolve, which still writes the other set."""
+        if self.m.world != 1 or not self.is_writer:
+            raise ValueError('rebind: world 1 writer only')
+        self.full = full
+        self._slabs = {t.t: {f: full[f][t.t] for f in self.fields} for t in self.m.mine}
+
     def post(self, k, after=None):
         """Round k: the k-th tile of every rank goes to the writer. after: an event (this rank's
         tile k complete) the send waits for instead of the work queued on the current stream."""

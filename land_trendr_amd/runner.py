@@ -199,8 +199,9 @@ class MosaicRunner:
             writes them while a later step's analyze does (a pixel deferred in one step but not
             in the next would otherwise keep the earlier step's value);
           * a runner of ONE tile alternates between two banks of its output planes (self.outs
-            names the bank the last step wrote): its next step writes the other bank, so its
-            analyze still runs beside the previous step's resolve;
+            names the bank the last step wrote; at world 1 also the label rasters,
+            self.exchange.full): its next step writes the other bank, so its analyze still runs
+            beside the previous step's resolve;
           * a caller that rewrites tile k's INPUT planes (bands, mask) between pipelined steps
             first makes its stream wait for tile_done(k): the previous step's resolve reads them.
         overlap=False after pipelined steps completes them first (finish())."""
@@ -321,15 +322,28 @@ class MosaicRunner:
         self._end_step(pending)
 
     def _flip_bank(self):
-        """A one-tile runner's pipelined step writes the other bank of its output planes (the
-        exchanged label slabs are shared: they are waited for through the tile's done event)."""
+        """A one-tile runner's pipelined step writes the other bank of its output planes. At
+        world 1 nothing is sent, so the label rasters alternate too (LabelExchange.rebind): the
+        step's analyze waits for nothing the previous step still runs, and its resolve overlaps
+        this step's analyze. At world > 1 the exchanged label slabs are shared by the banks: they
+        are waited for through the tile's done event."""
+        own = self.m.world == 1 and self.exchange.full is not None
         if len(self._banks) == 1:
             o = self._banks[0][0]
-            self._banks.append([{f: (x if f in self._ex_fields else torch.empty_like(x))
-                                 for f, x in o.items()}])
+            if own:
+                full1 = {f: torch.empty_like(x) for f, x in self.exchange.full.items()}
+                self._fulls = [self.exchange.full, full1]
+                t = self.items[0].tile.t
+                self._banks.append([{f: (full1[f][t] if f in self._ex_fields
+                                         else torch.empty_like(x)) for f, x in o.items()}])
+            else:
+                self._banks.append([{f: (x if f in self._ex_fields else torch.empty_like(x))
+                                     for f, x in o.items()}])
         self._bank ^= 1
         self.outs = self._banks[self._bank]
-        if any(f in self._ex_fields for f in self.outs[0]):
+        if own:
+            self.exchange.rebind(self._fulls[self._bank])
+        elif any(f in self._ex_fields for f in self.outs[0]):
             # the shared slabs: the other bank's last writer must be complete as well
             other = self._prev_done.get((self._bank ^ 1, 0))
             if other is not None:

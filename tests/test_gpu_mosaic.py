@@ -266,5 +266,13 @@ def test_pipelined_steps_with_changing_inputs_match_joined_steps(tiles):
             x, y = a.outs[k][f][..., :n], b.outs[k][f][..., :n]
             same = (x == y) | (torch.isnan(x) & torch.isnan(y)) if x.is_floating_point() else x == y
             assert bool(same.all()), (tiles, k, f, int((~same).sum()))
+    # the writer's label rasters (at world 1 a one-tile runner alternates two sets of them)
+    assert a.exchange.fields
+    for f in a.exchange.fields:
+        x, y = a.exchange.raster(f), b.exchange.raster(f)
+        assert bool((x == y).all()), (tiles, 'raster', f)
+    if tiles == 1:
+        assert a.exchange.full is a._fulls[a._bank]
+        assert a.outs[0]['class_val'].data_ptr() == a.exchange.full['class_val'][0].data_ptr()
     del a, b, a_items, b_items
     torch.cuda.empty_cache()
