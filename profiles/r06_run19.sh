@@ -3,7 +3,8 @@
 # _flip_bank + LabelExchange.rebind). Before, the label slabs were shared by the two banks, so a
 # step's analyze waited for the previous step's resolve (kernel trace of r06_fa: analyze starts
 # 53 us after the resolve ends, every step). (1) the pipelined-steps GPU tests; (2) c2 / c3 bench,
-# the product's resolve and the 3-waves-per-SIMD resolve (override code objects); (3) the default
+# the product's resolve (4 waves per SIMD, grid 4096) and the no-spill resolve at 3 and
+# 2 waves per SIMD (grids 3072 / 2048; override code objects, the latter by co_patch --vgprs 248); (3) the default
 # c2 command under rocprofv3 --kernel-trace: does the resolve now run beside the next analyze?
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/${1:-gpurun_out/r06_run19}
@@ -20,6 +21,8 @@ b() {  # name, env, args
 }
 b c2 "LT_NONE=1" "--config c2" && b c2_rw3 "LT_JIT_OVERRIDE_DIR=$R/build/override/rw3" "--config c2" && \
 b c3 "LT_NONE=1" "--config c3" && b c3_rw3 "LT_JIT_OVERRIDE_DIR=$R/build/override/rw3" "--config c3" && \
+b c2_rw2 "LT_JIT_OVERRIDE_DIR=$R/build/override/rw3v248" "--config c2" && \
+b c3_rw2 "LT_JIT_OVERRIDE_DIR=$R/build/override/rw3v248" "--config c3" && \
 b c2_again "LT_NONE=1" "--config c2" || exit 1
 cd /tmp
 timeout -k 10 220 rocprofv3 --kernel-trace --output-format csv -d $O/kt -o run -- python3 $R/bench.py --steps 5 --no-cpu-baseline --e2e-steps 0 --tiled-steps 0 > $O/c2_under_rocprof.json 2> $O/kt.err
