@@ -26,6 +26,7 @@ shuffle by label key into output_reducer, :128-152). Pixels are independent (SUR
 One process per GPU; torch.distributed is initialised by the caller (torchrun env). The same
 classes run over gloo on CPU tensors (tests/test_distributed.py).
 """
+import contextlib
 from dataclasses import dataclass
 
 import torch
@@ -101,11 +102,14 @@ class LabelExchange:
     queued on the current stream), wait() completes every posted one, raster(field) assembles
     the writer's [R, n_pix] raster in mosaic pixel order."""
 
-    def __init__(self, mosaic, spec, device, dist=None, dst=0):
+    def __init__(self, mosaic, spec, device, dist=None, dst=0, wire=None):
         """spec: {field: (rows, torch dtype)}, rows None for a [tile] plane (status) or the
-        plane count of a [rows, tile] field (R for label fields, Y for trendline fields)."""
+        plane count of a [rows, tile] field (R for label fields, Y for trendline fields).
+        wire: {field: torch dtype} a narrower type the field travels in (every value it holds
+        must fit: the caller's guarantee, runner.label_wire_types); the writer widens it back."""
         self.m, self.dist, self.dst = mosaic, dist, dst
         self.spec = dict(spec)
+        self.wire = {f: (wire or {}).get(f, self.spec[f][1]) for f in self.spec}
         self.fields = tuple(self.spec)
         self.device = torch.device(device)
         self.is_writer = mosaic.rank == dst
@@ -145,6 +149,8 @@ class LabelExchange:
                              if not self.is_writer and self.device.type == 'cuda' and
                              not self._staged and mosaic.world > 1 else None)
         self._works = []   # (round, work) in posting order
+        self._widen = []   # (wire buffer, raster slab): receives widened in wait()
+        self._wbufs = {}   # (tile, field) -> the writer's wire-type receive buffer
 
     def slab(self, tile):
         return self._slabs[tile.t]
@@ -166,6 +172,7 @@ class LabelExchange:
             return
         d = self.dist
         ops = []
+        widen = []  # (wire buffer, raster slab) pairs of this round's narrow receives
         if self.is_writer:
             for r in range(self.m.world):
                 if r == self.dst:
@@ -176,8 +183,12 @@ class LabelExchange:
                     for f in self.fields:
                         dst = self.full[f][t]
                         if self._staged:
-                            buf = torch.empty(dst.shape, dtype=dst.dtype)
+                            buf = torch.empty(dst.shape, dtype=self.wire[f])
                             self._staged_in.append((buf, dst))
+                            dst = buf
+                        elif self.wire[f] != dst.dtype:  # widened after the receive
+                            buf = self._wire_buf(t, f, dst)
+                            widen.append((buf, dst))
                             dst = buf
                         ops.append(d.P2POp(d.irecv, dst, r))
         else:
@@ -186,8 +197,19 @@ class LabelExchange:
                 s = self._slabs[mine[k].t]
                 if self._staged and after is not None:  # the host copy below waits for it
                     torch.cuda.current_stream(self.device).wait_event(after)
+                narrow = [f for f in self.fields if self.wire[f] != s[f].dtype]
+                packed = {}
+                if narrow:  # narrowed after the tile's kernels: on the send stream behind `after`
+                    # (into buffers kept per tile: this round's previous send of one completed
+                    # before the tile's kernels ran again, runner._wait_sends / wait())
+                    side = after is not None and self._send_stream is not None
+                    with torch.cuda.stream(self._send_stream) if side else contextlib.nullcontext():
+                        if side:
+                            self._send_stream.wait_event(after)
+                        t = mine[k].t
+                        packed = {f: self._wire_buf(t, f, s[f]).copy_(s[f]) for f in narrow}
                 for f in self.fields:
-                    src = s[f]
+                    src = packed.get(f, s[f])
                     if self._staged:  # a blocking copy: after the kernels queued so far
                         src = src.cpu()
                         self._staged_out.append(src)
@@ -196,6 +218,12 @@ class LabelExchange:
             if self._recv_stream is not None:
                 with torch.cuda.stream(self._recv_stream):
                     works = d.batch_isend_irecv(ops)
+                    if widen:  # stream-ordered: after the receives, before the next round's
+                        for w in works:
+                            w.wait()
+                        for buf, dst in widen:
+                            dst.copy_(buf)
+                        widen = []
             elif after is not None and self._send_stream is not None:
                 # RCCL's stream waits for the send stream, which waits for this tile alone
                 with torch.cuda.stream(self._send_stream):
@@ -204,6 +232,16 @@ class LabelExchange:
             else:
                 works = d.batch_isend_irecv(ops)
             self._works += [(k, w) for w in works]
+            self._widen += widen  # (no receive stream: widened in wait())
+
+    def _wire_buf(self, t, f, like):
+        """Tile t's field f in its wire type: the writer's receive buffer (a round's widening copy
+        is queued before the next round's receive into it) or a sender's send buffer."""
+        b = self._wbufs.get((t, f))
+        if b is None:
+            b = self._wbufs[(t, f)] = torch.empty(like.shape, dtype=self.wire[f],
+                                                   device=like.device)
+        return b
 
     def post_all(self):
         for k in range(self.m.rounds):
@@ -214,7 +252,13 @@ class LabelExchange:
             self._works.pop(0)[1].wait()
         for buf, dst in self._staged_in:
             dst.copy_(buf)
-        self._staged_in, self._staged_out = [], []
+        for buf, dst in self._widen:
+            dst.copy_(buf)
+        if self._recv_stream is not None and any(self.wire[f] != self.spec[f][1]
+                                                 for f in self.fields):
+            # the widening copies ran on the receive stream
+            torch.cuda.current_stream(self.device).wait_stream(self._recv_stream)
+        self._staged_in, self._staged_out, self._widen = [], [], []
 
     @property
     def can_overlap(self):

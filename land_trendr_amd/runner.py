@@ -23,6 +23,7 @@ from typing import Optional
 
 import torch
 
+from . import _abi
 from .distributed import LABEL_GATHER_FIELDS, LabelExchange
 from .engine import _DTYPE, _SHAPE_KIND
 
@@ -39,6 +40,22 @@ class TileInput:
     values: Optional[torch.Tensor]
     valid: Optional[torch.Tensor]      # [K, n] uint8 or None
     bands: Optional[torch.Tensor] = None  # [K, NB, n] band planes, or None (values given)
+
+
+def label_wire_types(params, fields):
+    """The narrower types the label planes travel to the writer in (LabelExchange wire), chosen
+    from what the kernels can write (lt_pixel.h RuleState1::write): onset_year a calendar year
+    (1-9999, a datetime.date's) or LT_NODATA, duration a year count (<= 255, lt_abi.h limits) or
+    LT_NODATA, class_val a rule's class value or LT_NODATA. Every such value fits int16 (class_val:
+    when the rules' values do), which narrows c2's 20 bytes per pixel and rule on the wire to 14
+    (magnitude stays binary64); the writer's rasters keep the API types. The choice depends on
+    the job's rules only, so every rank makes the same one."""
+    lo, hi = -(1 << 15), (1 << 15) - 1
+    w = {f: torch.int16 for f in ('onset_year', 'duration') if f in fields}
+    vals = [int(params.rules[r].class_val) for r in range(params.n_rules)] + [_abi.LT_NODATA]
+    if 'class_val' in fields and all(lo <= v <= hi for v in vals):
+        w['class_val'] = torch.int16
+    return w
 
 
 class MosaicRunner:
@@ -73,7 +90,8 @@ class MosaicRunner:
             return None if k == 'pix' else (R if k == 'rule' else Y)
 
         self.exchange = LabelExchange(mosaic, {f: (rows(f), _DTYPE[f]) for f in ex},
-                                      engine.device, dist, dst)
+                                      engine.device, dist, dst,
+                                      wire=label_wire_types(params, ex))
         W = mosaic.tile
         self.ring = max(0, int(ring))
         self._ring_last = {}  # ring slot -> (slab_free of its step, tile) of its last user

@@ -53,6 +53,8 @@ def _worker(rank, world, port, scene_px, tile, assign, result_path, dst=0, steps
     os.environ['MASTER_PORT'] = str(port)
     dist.init_process_group('gloo', rank=rank, world_size=world)
     r = _run(world, rank, scene_px, tile, assign, 7, dist, dst, steps, overlap)
+    # the label planes travel narrowed (runner.label_wire_types) and arrive widened, exactly
+    assert all(r.exchange.wire[f] == torch.int16 for f in ('class_val', 'onset_year', 'duration'))
     if overlap:  # the steps ran pipelined: some sends stayed in flight past their step
         assert r._overlap
     # bench.py's exchange check: the owners' per-tile checksums, all-reduced, equal the writer's
@@ -85,6 +87,20 @@ def _same(a, b):
     if a.dtype.kind == 'f':
         return (a.view(np.int64) == b.view(np.int64)).all()
     return (a == b).all()
+
+
+def test_label_wire_types_follow_the_rules_values():
+    """onset_year / duration always travel as int16; class_val only when every rule's value
+    (and LT_NODATA) fits, else in its API type; magnitude never narrows."""
+    from land_trendr_amd.runner import label_wire_types
+    from land_trendr_amd.settings import compile_params
+    p, _ = compile_params(10, RULES)
+    w = label_wire_types(p, ltd.LABEL_GATHER_FIELDS)
+    assert w == {'class_val': torch.int16, 'onset_year': torch.int16, 'duration': torch.int16}
+    big = [dict(RULES[0], val=40000)] + RULES[1:]
+    p2, _ = compile_params(10, big)
+    assert 'class_val' not in label_wire_types(p2, ltd.LABEL_GATHER_FIELDS)
+    assert label_wire_types(p, ('magnitude',)) == {}
 
 
 def test_tile_assignment_covers_mosaic_once():
