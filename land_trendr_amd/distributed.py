@@ -190,7 +190,7 @@ class LabelExchange:
                             buf = self._wire_buf(t, f, dst)
                             widen.append((buf, dst))
                             dst = buf
-                        ops.append(d.P2POp(d.irecv, dst, r))
+                        ops.append(d.P2POp(d.irecv, self._bytes(f, dst), r))
         else:
             mine = self.m.mine
             if k < len(mine):
@@ -213,7 +213,7 @@ class LabelExchange:
                     if self._staged:  # a blocking copy: after the kernels queued so far
                         src = src.cpu()
                         self._staged_out.append(src)
-                    ops.append(d.P2POp(d.isend, src, self.dst))
+                    ops.append(d.P2POp(d.isend, self._bytes(f, src), self.dst))
         if ops:
             if self._recv_stream is not None:
                 with torch.cuda.stream(self._recv_stream):
@@ -233,6 +233,11 @@ class LabelExchange:
                 works = d.batch_isend_irecv(ops)
             self._works += [(k, w) for w in works]
             self._widen += widen  # (no receive stream: widened in wait())
+
+    def _bytes(self, f, x):
+        """A narrowed field's buffer as the bytes the transport moves: RCCL (NCCL's type list)
+        has no 16-bit integer type, and the widening reads the buffer in its own type."""
+        return x.view(torch.uint8) if self.wire[f] != self.spec[f][1] else x
 
     def _wire_buf(self, t, f, like):
         """Tile t's field f in its wire type: the writer's receive buffer (a round's widening copy
