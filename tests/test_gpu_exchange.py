@@ -71,7 +71,7 @@ def _spec(R):
 
 @pytest.mark.parametrize('overlap', [False, True])
 def test_narrow_label_transfer_streams(overlap):
-    """Two tiles of rank 1 go to writer rank 0 over three steps with new labels each step; the
+    """Rank 1's tile goes to writer rank 0 in three steps, with new labels each step; the
     writer's rasters equal the sender's planes bit for bit after every step (joined), or after
     the last one (pipelined: the sender's next kernels wait only for that tile's last send)."""
     dev = torch.device('cuda', 0)
