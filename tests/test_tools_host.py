@@ -90,3 +90,28 @@ def test_co_patch_waitcnt_only_tightens_waits(tmp_path):
             else:
                 assert x == y
         assert n_wait > 0
+
+
+def test_co_audit_reads_descriptor_and_bounds(tmp_path):
+    """tools/co_audit.py (DESIGN.md § Wrong-result variants, round 6): the allocation it reads from
+    the kernel descriptor agrees with the code object's metadata, and a private array indexed by a
+    lane's own value shows up as a VGPR-addressed scratch access."""
+    sys.path.insert(0, os.path.join(ROOT, 'tools'))
+    import co_audit
+    import jit_isa
+    src = ('extern "C" __global__ void k(int* a, int n) {\n'
+           '  int t[40];\n'
+           '  for (int i = 0; i < 40; i++) t[(i * 7 + threadIdx.x) % 40] = i + n;\n'
+           '  a[threadIdx.x] = t[(threadIdx.x + n) % 40];\n}\n')
+    co = str(tmp_path / 'k.co')
+    with open(co, 'wb') as f:
+        f.write(jit_isa.hiprtc_compile(src))
+    desc = co_audit.descriptors(co)
+    notes = subprocess.check_output(['/opt/rocm/lib/llvm/bin/llvm-readelf', '--notes', co]).decode()
+    assert '.private_segment_fixed_size: %d' % desc['k']['private_segment'] in notes
+    assert '.vgpr_count:     %d' % desc['k']['vgprs'] in notes or desc['k']['vgprs'] % 8 == 0
+    asm = subprocess.check_output(['/opt/rocm/lib/llvm/bin/llvm-objdump', '-d', '--mcpu=gfx950',
+                                   co]).decode()
+    r = co_audit.audit_asm(asm, desc)['k']
+    assert r['vgpr_within'] and r['sgpr_within'] and r['scratch_const_within']
+    assert r['scratch_vgpr_addressed'], 'the dynamically indexed array lives in scratch'
