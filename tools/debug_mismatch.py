@@ -56,6 +56,16 @@ def main():
     ap.add_argument('--poison', default=None,
                     help='HEX[,HEX]: before step 1 (and 2) fill every SIMD\'s register file with '
                          'this 32-bit pattern (build/bin/libreg_poison.so, tools/reg_poison.hip)')
+    ap.add_argument('--stagger', default=None,
+                    help='START_MS,SPREAD_MS: before each step hold every wave slot for START_MS, '
+                         'then free the slots one by one over SPREAD_MS, so the launch\'s first '
+                         'generation of waves starts staggered (build/bin/libstagger.so, '
+                         'tools/stagger.hip)')
+    ap.add_argument('--hold', default=None,
+                    help='WAVES,MS,BIG: before each step start WAVES waves that keep their slots '
+                         'for MS (BIG 1: the variant\'s size, 128 VGPRs and its LDS; 0: a few '
+                         'VGPRs), so the step runs beside them; where they ran is reported '
+                         '(build/bin/libstagger.so, tools/stagger.hip)')
     a = ap.parse_args()
     pois = None
     if a.poison:
@@ -70,6 +80,49 @@ def main():
             rc = pl.lt_reg_poison(pats[k], 4096, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
             torch.cuda.synchronize()
             assert rc == 0, rc
+    if a.stagger:
+        import ctypes
+        import time
+        sl = ctypes.CDLL(os.path.join(ROOT, 'build', 'bin', 'libstagger.so'))
+        sl.lt_stagger.argtypes = [ctypes.c_int, ctypes.c_double, ctypes.c_double]
+        st_start, st_spread = (float(x) for x in a.stagger.split(','))
+        inner = pois
+
+        def pois(k):  # noqa: F811 (poison first, if asked, then the blocker)
+            if inner:
+                inner(k)
+            torch.cuda.synchronize()
+            rc = sl.lt_stagger(4096, st_start, st_spread)
+            assert rc == 0, rc
+            time.sleep(st_start / 2000.0)  # the blocker resident before the step is queued
+    hold_where = []
+    if a.hold:
+        import ctypes
+        import time
+        hl = ctypes.CDLL(os.path.join(ROOT, 'build', 'bin', 'libstagger.so'))
+        hl.lt_hold.argtypes = [ctypes.c_int, ctypes.c_double, ctypes.c_int]
+        h_waves, h_ms, h_big = a.hold.split(',')
+        h_waves, h_ms, h_big = int(h_waves), float(h_ms), int(h_big)
+        inner2 = pois
+
+        def pois(k):  # noqa: F811
+            if inner2:
+                inner2(k)
+            torch.cuda.synchronize()
+            rc = hl.lt_hold(h_waves, h_ms, h_big)
+            assert rc == 0, rc
+            time.sleep(0.005)  # the hold waves resident before the step is queued
+
+        def hold_report():
+            assert hl.lt_stagger_wait() == 0
+            ids = np.zeros(2 * h_waves, dtype=np.uint32)
+            assert hl.lt_hold_ids(ids.ctypes.data_as(ctypes.c_void_p), h_waves) == 0
+            hw, xcc = ids[0::2].astype(np.int64), ids[1::2].astype(np.int64) & 15
+            simd = (xcc << 16) | (((hw >> 13) & 7) << 8) | (((hw >> 12) & 1) << 7) | \
+                (((hw >> 8) & 15) << 2) | ((hw >> 4) & 3)
+            _, cnt = np.unique(simd, return_counts=True)
+            hold_where.append({'simds_used': int(len(cnt)),
+                               'waves_per_used_simd': np.bincount(cnt).tolist()})
     c = bench.CONFIGS[a.config]
     P = a.pixels or c['pixels']
     eng = get_engine(0)
@@ -80,17 +133,32 @@ def main():
     params, _ = compile_params(c['line_cost'], c['rules'], c['mode'])
     fn = eng.compile_index(IndexProgram('B1 - B2', band_dtype='int16'))
     r = MosaicRunner(eng, m, params, items, FIELDS, fn)
+    if a.stagger or a.hold:  # the module loaded and the buffers made before a blocked step is queued
+        r.step()
+        torch.cuda.synchronize()
+    import time as _t
+    step_s = []
     if pois:
         pois(0)
+    t = _t.perf_counter()
     r.step()
+    torch.cuda.current_stream().synchronize()  # the step's own work (not a blocker's)
+    step_s.append(_t.perf_counter() - t)
     torch.cuda.synchronize()
+    if a.hold:
+        hold_report()
     print('step 1 done', file=sys.stderr, flush=True)
     first = {f: r.outs[0][f].clone() for f in FIELDS}
     # determinism: the same launch again, every output plane compared bitwise with the first
     if pois:
         pois(1)
+    t = _t.perf_counter()
     r.step()
+    torch.cuda.current_stream().synchronize()  # the step's own work (not a blocker's)
+    step_s.append(_t.perf_counter() - t)
     torch.cuda.synchronize()
+    if a.hold:
+        hold_report()
     print('step 2 done', file=sys.stderr, flush=True)
     diff = torch.zeros(P, dtype=torch.bool, device=dev)
     for f in FIELDS:
@@ -155,6 +223,10 @@ def main():
     res['jit'] = {k: v for k, v in eng.jit_stats().items() if k != 'last_error'}
     res['jit_override_dir'] = os.environ.get('LT_JIT_OVERRIDE_DIR')
     res['poison'] = a.poison
+    res['stagger'] = a.stagger
+    res['hold'] = a.hold
+    res['hold_where'] = hold_where
+    res['step_wall_ms'] = [round(x * 1e3, 3) for x in step_s]
     print(json.dumps(res), flush=True)
 
 
