@@ -143,7 +143,17 @@ def patch_waitcnt(data, path, kind, lo=None, hi=None, kernels=None):
     return seen, changed
 
 
-def patch(src, dst, private, kernels=None, vgprs=None, waitcnt=None, rng=(None, None)):
+def patch_accum(data, accum, kernels, kds):
+    """COMPUTE_PGM_RSRC3 ACCUM_OFFSET (kd byte 44, bits 5:0, granules of 4): the first unified
+    register of the wave's AGPRs; the AGPR count is the allocation minus it."""
+    for k, off in kds.items():
+        if kernels is None or k in kernels:
+            r3 = struct.unpack('<I', data[off + 44:off + 48])[0]
+            r3 = (r3 & ~0x3f) | (accum // 4 - 1)
+            data[off + 44:off + 48] = struct.pack('<I', r3)
+
+
+def patch(src, dst, private, kernels=None, vgprs=None, waitcnt=None, rng=(None, None), accum=None):
     data = bytearray(open(src, 'rb').read())
     if waitcnt is not None:
         seen, changed = patch_waitcnt(data, src, waitcnt, rng[0], rng[1], kernels)
@@ -152,6 +162,8 @@ def patch(src, dst, private, kernels=None, vgprs=None, waitcnt=None, rng=(None, 
     done = []
     if vgprs is not None:
         patch_vgprs(data, names, vgprs, kernels, kd_offsets(src))
+    if accum is not None:
+        patch_accum(data, accum, kernels, kd_offsets(src))
     pos = data.find(KEY) if private is not None else -1
     while pos >= 0:
         # the owning kernel: the last `.name` before this key
@@ -187,6 +199,8 @@ def main():
     ap.add_argument('dst')
     ap.add_argument('--private', type=int, default=None, help='bytes per lane')
     ap.add_argument('--vgprs', type=int, default=None, help='VGPRs per lane (multiple of 8)')
+    ap.add_argument('--accum', type=int, default=None,
+                    help='ACCUM_OFFSET (multiple of 4): where the AGPRs start in the allocation')
     ap.add_argument('--kernel', action='append', default=None)
     ap.add_argument('--waitcnt', choices=sorted(WAIT_CLEAR), default=None,
                     help='set this counter of every s_waitcnt to 0 (stricter waits, same code)')
@@ -197,7 +211,7 @@ def main():
         lo, hi = a.range.split(':')
         rng = (int(lo, 16) if lo else None, int(hi, 16) if hi else None)
     done = patch(a.src, a.dst, a.private, set(a.kernel) if a.kernel else None, a.vgprs,
-                 a.waitcnt, rng)
+                 a.waitcnt, rng, a.accum)
     print('patched %s -> %s: private %s (%s), vgprs %s'
           % (a.src, a.dst, a.private, ', '.join('%s was %d' % d for d in done), a.vgprs))
 
