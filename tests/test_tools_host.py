@@ -115,3 +115,23 @@ def test_co_audit_reads_descriptor_and_bounds(tmp_path):
     r = co_audit.audit_asm(asm, desc)['k']
     assert r['vgpr_within'] and r['sgpr_within'] and r['scratch_const_within']
     assert r['scratch_vgpr_addressed'], 'the dynamically indexed array lives in scratch'
+
+
+def test_co_patch_accum_moves_only_the_agpr_split(tmp_path):
+    """co_patch.py --vgprs 136 --accum 136 (DESIGN.md § Wrong-result variants, run 25): the
+    descriptor's allocation and AGPR split change, the instructions do not."""
+    sys.path.insert(0, os.path.join(ROOT, 'tools'))
+    import co_audit
+    import jit_isa
+    src = 'extern "C" __global__ void k(double* a) { a[threadIdx.x] = a[threadIdx.x] * 3.0 + 1.0; }\n'
+    co = str(tmp_path / 'k.co')
+    with open(co, 'wb') as f:
+        f.write(jit_isa.hiprtc_compile(src))
+    out = str(tmp_path / 'p.co')
+    subprocess.check_call([sys.executable, os.path.join(ROOT, 'tools', 'co_patch.py'), co, out,
+                           '--vgprs', '136', '--accum', '136'], timeout=60)
+    d = co_audit.descriptors(out)['k']
+    assert d['vgprs'] == 136 and d['accum_offset'] == 136
+    dis = [subprocess.check_output(['/opt/rocm/lib/llvm/bin/llvm-objdump', '-d', '--mcpu=gfx950',
+                                    f]).decode().split('\n', 3)[3] for f in (co, out)]
+    assert dis[0] == dis[1]
