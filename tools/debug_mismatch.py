@@ -66,6 +66,11 @@ def main():
                          'for MS (BIG 1: the variant\'s size, 128 VGPRs and its LDS; 0: a few '
                          'VGPRs), so the step runs beside them; where they ran is reported '
                          '(build/bin/libstagger.so, tools/stagger.hip)')
+    ap.add_argument('--guard', default=None,
+                    help='WAVES,MS: before each step start WAVES guard waves (128 VGPRs each, '
+                         'filled with a pattern) that hold their slots for MS beside the step and '
+                         'report which of their registers changed (build/bin/libreg_guard.so, '
+                         'tools/reg_guard.hip)')
     a = ap.parse_args()
     pois = None
     if a.poison:
@@ -123,6 +128,46 @@ def main():
             _, cnt = np.unique(simd, return_counts=True)
             hold_where.append({'simds_used': int(len(cnt)),
                                'waves_per_used_simd': np.bincount(cnt).tolist()})
+    guard_found = []
+    if a.guard:
+        import ctypes
+        import time
+        gl = ctypes.CDLL(os.path.join(ROOT, 'build', 'bin', 'libreg_guard.so'))
+        gl.lt_reg_guard.argtypes = [ctypes.c_int, ctypes.c_double]
+        g_waves, g_ms = a.guard.split(',')
+        g_waves, g_ms = int(g_waves), float(g_ms)
+        inner3 = pois
+
+        def pois(k):  # noqa: F811
+            if inner3:
+                inner3(k)
+            torch.cuda.synchronize()
+            assert gl.lt_reg_guard(g_waves, g_ms) == 0
+            time.sleep(0.005)  # the guard waves resident before the step is queued
+
+        def guard_report():
+            assert gl.lt_reg_guard_wait() == 0
+            masks = np.zeros(4 * g_waves, dtype=np.uint32)
+            vals = np.zeros(16 * 64 * g_waves, dtype=np.uint32)
+            assert gl.lt_reg_guard_read(masks.ctypes.data_as(ctypes.c_void_p),
+                                        vals.ctypes.data_as(ctypes.c_void_p), g_waves) == 0
+            mk = masks.reshape(g_waves, 4).astype(np.uint64)
+            bits = [int(k) for k in range(128) if ((mk[:, k // 32] >> np.uint64(k % 32)) & np.uint64(1)).any()]
+            hit = (mk != 0).any(axis=1)
+            kept = list(range(8)) + list(range(120, 128))
+            v = vals.reshape(g_waves, 16, 64)
+            ex = []
+            for w in np.where(hit)[0][:4]:
+                for i, r in enumerate(kept):
+                    d = np.where(v[w, i] != (0xA5A50000 | r))[0]
+                    if len(d):
+                        ex.append({'wave': int(w), 'reg': 'v%d' % r, 'lanes': len(d),
+                                   'values': ['%08x' % x for x in v[w, i, d[:6]]]})
+            guard_found.append({'guard_waves_changed': int(hit.sum()), 'registers_changed': bits,
+                                'registers_changed_per_wave_hist': np.bincount(
+                                    [bin(int(m[0]) | int(m[1]) << 32 | int(m[2]) << 64 |
+                                         int(m[3]) << 96).count('1') for m in mk[hit]] or [0]).tolist(),
+                                'examples': ex[:16]})
     c = bench.CONFIGS[a.config]
     P = a.pixels or c['pixels']
     eng = get_engine(0)
@@ -133,7 +178,7 @@ def main():
     params, _ = compile_params(c['line_cost'], c['rules'], c['mode'])
     fn = eng.compile_index(IndexProgram('B1 - B2', band_dtype='int16'))
     r = MosaicRunner(eng, m, params, items, FIELDS, fn)
-    if a.stagger or a.hold:  # the module loaded and the buffers made before a blocked step is queued
+    if a.stagger or a.hold or a.guard:  # the module loaded and the buffers made before a blocked step is queued
         r.step()
         torch.cuda.synchronize()
     import time as _t
@@ -147,6 +192,8 @@ def main():
     torch.cuda.synchronize()
     if a.hold:
         hold_report()
+    if a.guard:
+        guard_report()
     print('step 1 done', file=sys.stderr, flush=True)
     first = {f: r.outs[0][f].clone() for f in FIELDS}
     # determinism: the same launch again, every output plane compared bitwise with the first
@@ -159,6 +206,8 @@ def main():
     torch.cuda.synchronize()
     if a.hold:
         hold_report()
+    if a.guard:
+        guard_report()
     print('step 2 done', file=sys.stderr, flush=True)
     diff = torch.zeros(P, dtype=torch.bool, device=dev)
     for f in FIELDS:
@@ -226,6 +275,8 @@ def main():
     res['stagger'] = a.stagger
     res['hold'] = a.hold
     res['hold_where'] = hold_where
+    res['guard'] = a.guard
+    res['guard_found'] = guard_found
     res['step_wall_ms'] = [round(x * 1e3, 3) for x in step_s]
     print(json.dumps(res), flush=True)
 
