@@ -136,6 +136,23 @@ def main():
         w, _, _, _ = lockstep(keep)
         res['budget'][str(B)] = {'deferred_frac': round(1 - len(keep) / len(Ks), 4),
                                  'wave_starts_per_column': round(w, 3)}
+    # pixels regrouped into waves by a per-pixel key within blocks of G consecutive pixels (a
+    # workgroup that sorts its pixels in LDS before the DP): the key 'total' is the lane's own
+    # starts over all columns (known only after the DP: the bound of any such regrouping), the
+    # others computable before it
+    def rough(i):
+        y = np.asarray(series[i][1], float)
+        return float(np.sum((y[2:] - 2 * y[1:-1] + y[:-2]) ** 2)) if len(y) >= 3 else 0.0
+    keys = {'total': lambda i: float(Ks[i].sum()) if len(Ks[i]) else 0.0,
+            'roughness': rough, 'points': lambda i: float(len(series[i][1]))}
+    res['sorted_blocks'] = {}
+    for name, key in keys.items():
+        for G in (256, 1024):
+            order = []
+            for g0 in range(0, len(Ks), G):
+                order += sorted(range(g0, min(len(Ks), g0 + G)), key=key)
+            res['sorted_blocks']['%s_G%d' % (name, G)] = round(
+                lockstep([Ks[i] for i in order])[0], 3)
     print(json.dumps(res))
 
 
