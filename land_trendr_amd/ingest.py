@@ -393,11 +393,17 @@ def ingest_stack(rast_fns, grid, mask_fns=None, bands=None, threads=None, pixels
                 ranges=ranges)
 
 
+def stack_offset(stack, p0, p1):
+    """Where grid points p0..p1 of an ingest_stack result sit in its gathered arrays (the last
+    axis): they must lie inside one of the ranges it gathered."""
+    for a, b, q0 in stack.get('ranges', [(0, stack['n_pix'], 0)]):
+        if a <= p0 and p1 <= b:
+            return q0 + p0 - a
+    raise KeyError('grid points %d..%d were not gathered by this rank' % (p0, p1))
+
+
 def stack_range(stack, p0, p1):
     """The (bands [K, nb, n], valid [K, n]) views of grid points p0..p1 of an ingest_stack
     result: they must lie inside one of the ranges it gathered."""
-    for a, b, q0 in stack.get('ranges', [(0, stack['n_pix'], 0)]):
-        if a <= p0 and p1 <= b:
-            q = q0 + p0 - a
-            return stack['bands'][:, :, q:q + p1 - p0], stack['valid'][:, q:q + p1 - p0]
-    raise KeyError('grid points %d..%d were not gathered by this rank' % (p0, p1))
+    q = stack_offset(stack, p0, p1)
+    return stack['bands'][:, :, q:q + p1 - p0], stack['valid'][:, q:q + p1 - p0]

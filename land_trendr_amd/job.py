@@ -34,13 +34,14 @@ import argparse
 import json
 import os
 import sys
+import time
 
 import numpy as np
 
 from . import _abi
 from .geotiff import GeoTiff
 from .ingest import (analysis_rasters, grid_axes, grid_coords, grid_offsets, ingest_stack,
-                     mask_name, rast2grid, rast_local, read_grid, stack_range)
+                     mask_name, rast2grid, rast_local, read_grid, stack_offset, stack_range)
 
 IN_SETTINGS = '%s/input/settings.json'
 IN_RASTS = '%s/input/rasters/'
@@ -213,21 +214,48 @@ class LocalJob:
         if (m.world, m.rank, m.scene_pixels) != (world, rank, [P]):
             raise RuntimeError('parse() ran under another process group')
         K, Y = self.scene.n_obs, self.scene.n_years
+        t_in = time.perf_counter()
+        # LT_JOB_UPLOAD 'whole' (default on a GPU): the rank's gathered stack (its tiles' pixel
+        # ranges) crosses to the device in one copy per array and each tile's inputs are made from
+        # device views of it; 'tile': each tile's bands gathered into a host copy first (a 2 GB
+        # single-threaded copy per 16.8 Mpx tile, most of round 6's job analysis time)
+        whole = (cuda and os.environ.get('LT_JOB_UPLOAD', 'whole') == 'whole' and
+                 st['bands'].flags.c_contiguous and st['valid'].flags.c_contiguous and
+                 st['bands'].nbytes + st['valid'].nbytes <= (64 << 30))
+        if whole:
+            w_bands = torch.from_numpy(st['bands']).to(dev)
+            if slots != list(range(st['bands'].shape[1])):
+                w_bands = w_bands[:, slots]
+            w_valid = torch.from_numpy(st['valid']).to(dev)
         items = []
         for t in m.mine:
-            t_bands, t_valid = stack_range(st, t.p0, t.p1)
-            bands = torch.from_numpy(np.ascontiguousarray(t_bands[:, slots])).to(dev)
+            if whole:
+                q = stack_offset(st, t.p0, t.p1)
+                bands = w_bands[:, :, q:q + t.n]
+                valid = w_valid[:, q:q + t.n]
+            else:
+                t_bands, t_valid = stack_range(st, t.p0, t.p1)
+                bands = torch.from_numpy(np.ascontiguousarray(t_bands[:, slots])).to(dev)
+                valid = torch.from_numpy(np.ascontiguousarray(t_valid)).to(dev)
             if cuda and fn.lin is not None and len(slots) == 2 and bands.dtype == torch.int16:
                 # the fused load stage reads a pixel's two int16 bands as one 32-bit word
                 inter = torch.empty((K, t.n, 2), dtype=bands.dtype, device=dev).permute(0, 2, 1)
                 inter.copy_(bands)
                 bands = inter
-            valid = torch.from_numpy(np.ascontiguousarray(t_valid)).to(dev)
+            elif whole:
+                bands = bands.contiguous()
+            if whole:
+                valid = valid.contiguous()
             if cuda:  # the winner pick reads the mask as bit planes (one word per 32 obs)
                 valid = pack_valid_bits(valid)
             # the index raster: allocated by the runner only if the load kernel writes it (the
             # fused load stage never does)
             items.append(TileInput(t, self.scene, None, valid, bands))
+        if whole:
+            del w_bands, w_valid  # every tile holds its own copies
+        if cuda:
+            torch.cuda.synchronize(dev)
+        self.analyze_s = {'inputs': time.perf_counter() - t_in}
         host = self.host_trendline = self._trendline_planes(tl_fields, Y, P, dist, world, rank)
         # the trendline planes: a ring of three tiles' buffers on the GPU (tile k reuses tile
         # k-3's once its rows have reached the host), so a rank's HBM never holds all its tiles'
@@ -260,6 +288,7 @@ class LocalJob:
             copied[k] = tls.push({f: runner.outs[k][f] for f in tl_fields}, t.n, t)
 
         # tile k-1's rows are queued behind tile k's kernels, so the copies overlap them
+        t_st = time.perf_counter()
         try:
             runner.step(after_tile=(lambda k: push(k - 1) if k > 0 else None) if cuda else None,
                         slab_free=copied.get if cuda else None)
@@ -274,7 +303,10 @@ class LocalJob:
             if items:
                 push(len(items) - 1)
             torch.cuda.synchronize(dev)
+            self.analyze_s['steps'] = time.perf_counter() - t_st
+            t_dr = time.perf_counter()
             tls.drain()
+            self.analyze_s['drain'] = time.perf_counter() - t_dr
         else:  # a CPU engine (tests): its planes are host tensors already
             for o, it in zip(runner.outs, items):
                 for f in tl_fields:
