@@ -130,11 +130,17 @@ class GeoTiff:
         except ValueError as e:
             raise TiffError(str(e))
 
-    def read(self, threads=None, native=True):
+    def read(self, threads=None, native=True, out=None):
         """All bands as a [bands, rows, cols] array in the sample type (native byte order).
         Strip-organised LZW / uncompressed images with integer predictors are decoded on
-        `threads` threads by liblt_io.so (default: the host's share, ingest.host_threads);
-        native=False takes the per-strip path (tests compare the two)."""
+        `threads` threads by liblt_io.so (default: the host's share, ingest.host_threads), into
+        `out` when given (a C-contiguous array of that shape and type; the other paths copy into
+        it); native=False takes the per-strip path (tests compare the two)."""
+        if out is not None and not (native and 273 in self.tags and tiffcodec.native_strips(
+                self.compression, self.predictor, self.bits) and (
+                self.predictor == 1 or self.dtype.kind in 'iu')):
+            out[...] = self.read(threads, native)
+            return out
         t = self.tags
         W, H, B = self.width, self.height, self.bands
         spp = B if self.planar == 1 else 1
@@ -147,7 +153,7 @@ class GeoTiff:
             try:
                 return tiffcodec.decode_strips(self._d, t[273], t[279], self.compression,
                                                self.predictor, self.dtype, self._bo == '>', W, H,
-                                               B, self.planar, rps, threads)
+                                               B, self.planar, rps, threads, out=out)
             except ValueError as e:
                 raise TiffError(str(e))
         if 273 in t:  # strips

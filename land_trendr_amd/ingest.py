@@ -363,10 +363,15 @@ def ingest_stack(rast_fns, grid, mask_fns=None, bands=None, threads=None, pixels
         if max(numbers) > ds.bands:
             raise Exception('Band %s requested but raster only has %s bands' % (max(numbers),
                                                                                  ds.bands))
-        planes = ds.read(threads=per_file).reshape(ds.bands, -1)
         idx, ok, ident = offsets(ds)
-        src = planes[sel] if sel != list(range(ds.bands)) else planes
-        take(src, idx, ok, ident, out_bands[k])
+        if (ident and idx is None and sel == list(range(ds.bands)) and len(spans) == 1 and
+                spans[0][:2] == (0, P) and ds.width * ds.height == P):
+            # raster order, every band, one full range: decoded in place (no copy of the planes)
+            ds.read(threads=per_file, out=out_bands[k].reshape(ds.bands, ds.height, ds.width))
+        else:
+            planes = ds.read(threads=per_file).reshape(ds.bands, -1)
+            src = planes[sel] if sel != list(range(ds.bands)) else planes
+            take(src, idx, ok, ident, out_bands[k])
         if ok is not None and not ident:
             out_bands[k][:, ~ok] = 0
         v = valid[k]

@@ -138,10 +138,17 @@ def native_strips(compression, predictor, bits):
 
 
 def decode_strips(buf, offsets, counts, compression, predictor, dtype, big_endian, width, height,
-                  bands, planar, rows_per_strip, threads):
+                  bands, planar, rows_per_strip, threads, out=None):
     """Every strip of a strip-organised image, decoded on `threads` threads (liblt_io.so
-    lt_tiff_decode_strips) -> [bands, height, width] in native byte order."""
-    out = np.empty((bands, height, width), np.dtype(dtype).newbyteorder('='))
+    lt_tiff_decode_strips) -> [bands, height, width] in native byte order (into `out`, a C-contiguous
+    array of that shape and type, when given)."""
+    want = np.dtype(dtype).newbyteorder('=')
+    if out is None:
+        out = np.empty((bands, height, width), want)
+    elif (out.shape != (bands, height, width) or out.dtype != want or
+          not out.flags.c_contiguous or not out.flags.writeable):
+        raise ValueError('decode_strips: out must be a writable C-contiguous %s array of shape %s'
+                         % (want, (bands, height, width)))
     offs = np.ascontiguousarray(offsets, np.uint64)
     cnts = np.ascontiguousarray(counts, np.uint64)
     src = np.frombuffer(buf, np.uint8)

@@ -216,6 +216,14 @@ def test_native_strip_decode_matches_per_strip_path(tmp_path, dtype, bo, planar,
     for threads in (1, 3):
         got = g.read(threads=threads)
         assert got.dtype == want.dtype and np.array_equal(got, want)
+    # decoded in place into a caller's array (ingest_stack's raster-order path), and refused
+    # for a wrongly shaped one
+    buf = np.full(want.shape, 77, want.dtype)
+    assert g.read(threads=2, out=buf) is buf and np.array_equal(buf, want)
+    with pytest.raises(ValueError):
+        tiffcodec.decode_strips(g._d, g.tags[273], g.tags[279], g.compression, g.predictor,
+                                g.dtype, g._bo == '>', 7, 11, 3, g.planar, 4, 1,
+                                out=np.empty((3, 7, 11), want.dtype))
 
 
 def test_native_strip_encode_matches_per_strip_encoder(tmp_path):
