@@ -8,6 +8,8 @@ uint/int/float of 8/16/32/64 bits, plus the GeoTIFF/GDAL tags kept as raw values
 (ModelPixelScale, ModelTiepoint, GeoKeyDirectory, GDAL_NODATA). Returns numpy arrays in the
 file's sample type, [bands, rows, cols] — what `ds2array(ds, b)` gives per band.
 """
+import mmap
+import os
 import struct
 
 import numpy as np
@@ -29,7 +31,15 @@ class TiffError(ValueError):
 class GeoTiff:
     def __init__(self, path):
         with open(path, 'rb') as f:
-            self._d = f.read()
+            # mapped, not read: the strip decoder reads the compressed strips where the page cache
+            # holds them (a read() copied every 174 MB raster of a c2-size stack once more)
+            # (LT_TIFF_MMAP=0: read, for A/B runs)
+            try:
+                if os.environ.get('LT_TIFF_MMAP', '1') == '0':
+                    raise ValueError
+                self._d = mmap.mmap(f.fileno(), 0, access=mmap.ACCESS_READ)
+            except (ValueError, OSError):  # an empty or unmappable file
+                self._d = f.read()
         d = self._d
         if d[:2] == b'II':
             self._bo = '<'
