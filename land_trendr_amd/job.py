@@ -65,13 +65,39 @@ class LocalJob:
         self.on_error = on_error
         self.work_dir = work_dir or os.path.join(root, job, 'work')
         self.settings_path = os.path.join(root, IN_SETTINGS % job)
-        self.grid_fn = os.path.join(root, OUT_GRID % job)
+        self._grid_fn = os.path.join(root, OUT_GRID % job)
+        self._grid_writer = None  # (thread, [exception]) writing the grid CSV beside parse()
         self.out_dir = os.path.join(root, OUT_RASTS % job)
         self.engine = engine
         self._host = None
         self.host_trendline = None
-        self.order = None        # grid point of each internal pixel (None: grid order)
+        self._order = None       # grid point of each internal pixel (None: grid order)
+        self._raster_hw = None   # (rows, cols) of the raster order, or None
         self.raster_grid = None  # (geotransform, rows, cols) of the raster order, or None
+
+    @property
+    def grid_fn(self):
+        """The grid CSV (the reference's grid file): complete once this returns (a one-rank
+        job's setup writes it on a thread of its own while parse runs)."""
+        self._join_grid()
+        return self._grid_fn
+
+    def _join_grid(self):
+        w, self._grid_writer = self._grid_writer, None
+        if w is not None:
+            w[0].join()
+            if w[1]:
+                raise w[1][0]
+
+    @property
+    def order(self):
+        """Grid point of each internal pixel (raster order), None in grid order: pixel (row r,
+        column c) is grid point c * rows + r, made on first use (49 M entries at c2 size)."""
+        if self._order is None and self._raster_hw is not None:
+            H, W = self._raster_hw
+            self._order = ((np.arange(W, dtype=np.int64) * H)[None, :] +
+                           np.arange(H, dtype=np.int64)[:, None]).ravel()
+        return self._order
 
     def _path(self, key):
         return os.path.join(self.root, key)
@@ -99,17 +125,35 @@ class LocalJob:
         dist, _, rank = self._dist()
         if rank == 0:
             self._locate(rdir, rasts)
-            os.makedirs(os.path.dirname(self.grid_fn), exist_ok=True)
-            tmp = '%s.tmp%d' % (self.grid_fn, os.getpid())
-            rast2grid(self.rast_fns[0], out_csv=tmp)
-            os.replace(tmp, self.grid_fn)
+            os.makedirs(os.path.dirname(self._grid_fn), exist_ok=True)
+            tmp = '%s.tmp%d' % (self._grid_fn, os.getpid())
+
+            def write_grid(err):
+                try:
+                    rast2grid(self.rast_fns[0], out_csv=tmp)
+                    os.replace(tmp, self._grid_fn)
+                except BaseException as e:  # re-raised by the first grid_fn access
+                    err.append(e)
+            self._join_grid()
+            err = []
+            if dist is None:  # one rank: no other process waits for the file
+                import threading
+                th = threading.Thread(target=write_grid, args=(err,), daemon=True)
+                th.start()
+                self._grid_writer = (th, err)
+            else:
+                write_grid(err)
+                if err:
+                    raise err[0]
         if dist is not None:
             dist.barrier()
         if rank != 0:
             self._locate(rdir, rasts)  # every archive is extracted by now: only listed
-        # the grid's point coordinates, as parsing the CSV just written gives them
-        self.grid_xy = grid_coords(self.rast_fns[0])
+        # the grid's point coordinates, as parsing the CSV being written gives them (raster
+        # order: made from the template's axes)
         self._internal_order()
+        if self._raster_hw is None:
+            self.grid_xy = grid_coords(self.rast_fns[0])
         with open(self.settings_path) as f:
             self.settings = json.load(f)
         return self.rast_fns
@@ -126,7 +170,7 @@ class LocalJob:
         pt2val's addressing (grid_offsets' operations) on the grid's distinct coordinates: the
         offsets of a column's points depend on its x alone, a row's on its y. The grid CSV keeps
         the reference's order; grid_wkts() gives the WKTs in the internal order."""
-        self.order = None
+        self._order = self._raster_hw = None
         self.raster_grid = None
         tmpl = GeoTiff(self.rast_fns[0])
         H, W = tmpl.height, tmpl.width
@@ -136,8 +180,7 @@ class LocalJob:
         yo = np.trunc((yv - gt[3]) * 1.0 / gt[5])
         if not (np.array_equal(xo, np.arange(W)) and np.array_equal(yo, np.arange(H))):
             return  # some point not on its own pixel: grid order, offsets per point
-        q = np.arange(H * W, dtype=np.int64)
-        self.order = (q % W) * H + q // W  # pixel (row r, column c) is grid point c * H + r
+        self._raster_hw = (H, W)  # self.order: pixel (row r, column c) is grid point c * H + r
         self.grid_xy = (np.tile(xv, H), np.repeat(yv, W))
         self.raster_grid = (gt, H, W)
 
@@ -388,7 +431,7 @@ class LocalJob:
         tmpl = GeoTiff(self.rast_fns[0])
         rows, cols = tmpl.height, tmpl.width
         lng, lat = self.grid_xy
-        if self.order is not None:  # raster order: internal pixel q is template pixel q
+        if self._raster_hw is not None:  # raster order: internal pixel q is template pixel q
             dest, ok = np.arange(rows * cols, dtype=np.int64), np.ones(rows * cols, bool)
         else:
             dest, ok = grid_offsets(tmpl.geotransform(), (rows, cols), lng, lat)
@@ -404,7 +447,7 @@ class LocalJob:
         self._host = None
         names = [d.strftime('%Y-%m-%d') for d in self.scene.dates]
         cuda = torch.device(self.engine.device).type == 'cuda'
-        distinct = self.order is not None or np.bincount(dest, minlength=rows * cols).max() <= 1
+        distinct = self._raster_hw is not None or np.bincount(dest, minlength=rows * cols).max() <= 1
         if cuda and distinct and len(set(names)) == len(names):
             ddest = torch.from_numpy(np.ascontiguousarray(dest, np.int64)).to(dp['status'].device)
             out = {}
@@ -439,8 +482,11 @@ class LocalJob:
         self.setup()
         self.parse()
         if self.analyze() is None:
+            self._join_grid()
             return None
-        return self.output()
+        out = self.output()
+        self._join_grid()
+        return out
 
 
 class _DeviceRows:

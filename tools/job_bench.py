@@ -191,7 +191,7 @@ def main():
                'parse_mpx_per_s': round(P / t['parse'] / 1e6, 2),
                'analyze_mpx_per_s': round(P / t['analyze'] / 1e6, 2),
                'output_rasters': len(files), 'output_bytes': out_bytes,
-               'raster_order': j.order is not None,
+               'raster_order': j._raster_hw is not None,
                'jit': getattr(j, 'jit_stats', None),
                'analyze_parts_s': {k: round(v, 3) for k, v in getattr(j, 'analyze_s', {}).items()},
                'upload': os.environ.get('LT_JOB_UPLOAD', 'whole')}
