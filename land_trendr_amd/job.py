@@ -462,6 +462,7 @@ class LocalJob:
                 rows_dev = _DeviceRows(self.host_trendline, dp['status'].device)
                 trendline_rasters_device(self.engine, rows_dev, self.scene, self.scene.dates,
                                          (rows, cols), ddest, tdt, self.raster_mode, sink=write)
+            self._join_grid()  # the grid CSV, the job's other output, in place too
             return out
         n = rows * cols
         placed = {}
@@ -474,7 +475,9 @@ class LocalJob:
         if self.trendline:
             rasters.update(trendline_rasters(placed, self.scene, self.scene.dates, (rows, cols),
                                              tdt, self.raster_mode))
-        return dict(output_reducer(rasters, tmpl, self.root, self.job))
+        res = dict(output_reducer(rasters, tmpl, self.root, self.job))
+        self._join_grid()
+        return res
 
     def run(self):
         """Every rank runs setup/parse/analysis; the writer (rank 0) also writes the rasters.
