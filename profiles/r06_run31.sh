@@ -1,5 +1,5 @@
 #!/bin/bash
-# r06 run 31: the c2-size job with the grid CSV written beside parse and the raster order made lazily (GPU job tests first)
+# r06 run 31 (output() joins the grid writer): the c2-size job with the grid CSV written beside parse and the raster order made lazily (GPU job tests first)
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/${1:-gpurun_out/r06_run31}
 mkdir -p $O
