@@ -320,8 +320,27 @@ class LocalJob:
             eng.set_jit_mode(True)
             runner.prepare_jit(wait=False)
 
+        # a completed year row of tile t, copied from its pinned ring buffer into the host plane
+        # in pieces on a pool of host threads (numpy releases the GIL for the copy): one thread
+        # copied ~10 GB/s, the bound of a trendline job's analysis (profiles/r06_run33); the ring
+        # buffer is reused only after sink() returns
+        from concurrent.futures import ThreadPoolExecutor
+        from .ingest import host_threads
+        n_cp = max(1, min(8, host_threads()))
+        pool = ThreadPoolExecutor(n_cp) if cuda and n_cp > 1 else None
+
         def sink(f, row, view, t):  # one completed year row of tile t
-            host[f][row, t.p0:t.p1] = view.numpy().view(host[f].dtype)
+            src = view.numpy().view(host[f].dtype)
+            dst = host[f][row, t.p0:t.p1]
+            n = src.shape[0]
+            if pool is None or n < (1 << 20):
+                dst[...] = src
+                return
+            step = -(-n // n_cp)
+
+            def piece(a):
+                dst[a:a + step] = src[a:a + step]
+            list(pool.map(piece, range(0, n, step)))
 
         tls = TrendlineStream(m.tile * 8, dev, depth=16, sink=sink) if cuda else None
         copied = {}  # tile -> event after its rows' D2H copies
@@ -350,6 +369,8 @@ class LocalJob:
             t_dr = time.perf_counter()
             tls.drain()
             self.analyze_s['drain'] = time.perf_counter() - t_dr
+        if pool is not None:
+            pool.shutdown()
         else:  # a CPU engine (tests): its planes are host tensors already
             for o, it in zip(runner.outs, items):
                 for f in tl_fields:
