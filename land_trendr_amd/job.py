@@ -472,17 +472,35 @@ class LocalJob:
         if cuda and distinct and len(set(names)) == len(names):
             ddest = torch.from_numpy(np.ascontiguousarray(dest, np.int64)).to(dp['status'].device)
             out = {}
+            # each raster is encoded and written on a writer thread (its LZW strips on the native
+            # pool) while the next one is assembled on the GPU and copied back: at most three in
+            # flight; written in key order, the first error re-raised
+            from collections import deque
+            from concurrent.futures import ThreadPoolExecutor
+            writer = ThreadPoolExecutor(1)
+            inflight = deque()
+
+            def settle(keep):
+                while len(inflight) > keep:
+                    out.update(inflight.popleft().result())
 
             def write(key, arr):  # each raster to its file as soon as it is on the host
-                out.update(output_reducer({key: arr}, tmpl, self.root, self.job))
+                inflight.append(writer.submit(
+                    lambda r: dict(output_reducer(r, tmpl, self.root, self.job)), {key: arr}))
+                settle(2)
 
-            for k, a in label_rasters_device(self.engine, dp, self.rules, (rows, cols), ddest,
-                                             tdt, self.raster_mode).items():
-                write(k, a)
-            if self.trendline:
-                rows_dev = _DeviceRows(self.host_trendline, dp['status'].device)
-                trendline_rasters_device(self.engine, rows_dev, self.scene, self.scene.dates,
-                                         (rows, cols), ddest, tdt, self.raster_mode, sink=write)
+            try:
+                for k, a in label_rasters_device(self.engine, dp, self.rules, (rows, cols), ddest,
+                                                 tdt, self.raster_mode).items():
+                    write(k, a)
+                if self.trendline:
+                    rows_dev = _DeviceRows(self.host_trendline, dp['status'].device)
+                    trendline_rasters_device(self.engine, rows_dev, self.scene, self.scene.dates,
+                                             (rows, cols), ddest, tdt, self.raster_mode,
+                                             sink=write)
+                settle(0)
+            finally:
+                writer.shutdown(wait=True)
             self._join_grid()  # the grid CSV, the job's other output, in place too
             return out
         n = rows * cols
