@@ -177,3 +177,20 @@ def test_job_setup_errors(tmp_path):
     with pytest.raises(Exception, match='No analysis rasters'):
         LocalJob(str(tmp_path), 'j').setup()
     shutil.rmtree(tmp_path / 'j')
+
+
+def test_grid_csv_writer_thread_reraises(tmp_path, monkeypatch):
+    """A one-rank setup() writes the grid CSV on a thread beside parse(); a failure there reaches
+    the caller at the first grid_fn access (and at output()), not silently."""
+    import land_trendr_amd.job as jobmod
+    root = str(tmp_path / 'job')
+    make_job(root)
+
+    def broken(*a, **k):
+        raise OSError('disk full')
+    monkeypatch.setattr(jobmod, 'rast2grid', broken)
+    j = LocalJob(root, 'synth')
+    j.setup()  # returns: the grid is still being written
+    with pytest.raises(OSError, match='disk full'):
+        j.grid_fn
+    assert os.path.basename(j.grid_fn)  # joined once: the path itself afterwards
