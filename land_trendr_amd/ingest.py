@@ -292,24 +292,6 @@ class _Offsets:
         return hit
 
 
-def host_empty(shape, dtype):
-    """np.empty for the stack's large host planes, backed by anonymous memory advised for
-    transparent huge pages (LT_HOST_HUGEPAGES=0: plain np.empty): the decode threads' first
-    touch of a c2-size stack is then ~3k page faults instead of ~1.4 M."""
-    dtype = np.dtype(dtype)
-    n = int(np.prod(shape)) * dtype.itemsize
-    if n < (64 << 20) or os.environ.get('LT_HOST_HUGEPAGES', '1') == '0':
-        return np.empty(shape, dtype)
-    import mmap
-    try:
-        mm = mmap.mmap(-1, n, flags=mmap.MAP_PRIVATE | mmap.MAP_ANONYMOUS)
-        if hasattr(mmap, 'MADV_HUGEPAGE'):
-            mm.madvise(mmap.MADV_HUGEPAGE)
-    except (OSError, ValueError, AttributeError):
-        return np.empty(shape, dtype)
-    return np.frombuffer(mm, dtype, int(np.prod(shape))).reshape(shape)
-
-
 def ingest_stack(rast_fns, grid, mask_fns=None, bands=None, threads=None, pixels=None,
                  raster_grid=None):
     """parse_mapper over every analysis raster, as planes for analysis_reducer_batch.
@@ -354,8 +336,8 @@ def ingest_stack(rast_fns, grid, mask_fns=None, bands=None, threads=None, pixels
     first = _open(rast_fns[0])
     numbers = list(bands) if bands is not None else list(range(1, first.bands + 1))
     dtype = first.dtype.newbyteorder('=')
-    out_bands = host_empty((K, len(numbers), Q), dtype)
-    valid = host_empty((K, Q), np.uint8)
+    out_bands = np.empty((K, len(numbers), Q), dtype)
+    valid = np.empty((K, Q), np.uint8)
     offsets = _Offsets(lng, lat, raster_grid)
     sel = [b - 1 for b in numbers]
     spans = [(p0, p1, q0) for p0, p1, q0 in ranges]

@@ -396,8 +396,7 @@ class LocalJob:
         from .engine import _DTYPE
         np_dt = {f: np.dtype(str(_DTYPE[f]).replace('torch.', '')) for f in fields}
         if world == 1:
-            from .ingest import host_empty
-            return {f: host_empty((Y, P), np_dt[f]) for f in fields}
+            return {f: np.empty((Y, P), np_dt[f]) for f in fields}
         d = os.path.join(self.work_dir, 'trendline')
         path = {f: os.path.join(d, f + '.bin') for f in fields}
         if rank == 0:
