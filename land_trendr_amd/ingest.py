@@ -389,8 +389,12 @@ def ingest_stack(rast_fns, grid, mask_fns=None, bands=None, threads=None, pixels
     total = threads or host_threads()
     # a few files at a time, each file's strips on its share of the threads (lt_tiff_decode_strips
     # balances thousands of strips; one thread per file left half the workers idle in the last
-    # round of a 30-file stack)
-    n = max(1, min(K, total, max(1, total // 4)))
+    # round of a 30-file stack): two threads per file, eight files at once on 16 threads (the
+    # c2-size job's parse 1.26 s against 1.36-1.38 with four threads per file and 1.29 with one,
+    # profiles/r06_run43)
+    n = max(1, min(K, total, max(1, total // 2)))
+    if os.environ.get('LT_INGEST_FILES'):  # files decoded at once (A/B runs)
+        n = max(1, min(K, total, int(os.environ['LT_INGEST_FILES'])))
     per_file = max(1, total // n)
     with ThreadPoolExecutor(n) as pool:
         dates = list(pool.map(one, range(K)))
