@@ -55,23 +55,35 @@ extern "C" {
 int64_t lt_lzw_decode(const uint8_t* in, int64_t n_in, uint8_t* out, int64_t cap) {
   if (!in || n_in < 0 || (cap > 0 && !out)) return LT_IO_ERR_ARG;
   if (cap >= (int64_t)1 << 31) return LT_IO_ERR_ARG;  // strips are far smaller (32-bit positions)
-  // Every string of the table is already in `out`: code c >= kFirst is the len[c] bytes at
-  // out[pos[c]] (where it was last written), so emitting is a copy from earlier output and a new
-  // entry is (the previous emission's position, its length + 1): no per-byte chain walk. The
-  // table lives on the stack (a thread_local one in a -fPIC library costs a __tls_get_addr call
-  // per access).
-  uint32_t pos[4096];
+  // Every string of the table is already in `out`: code c >= kFirst is the len[c] bytes at src[c]
+  // (where it was last written), so emitting is a copy from earlier output and a new entry is
+  // (the previous emission's start, its length + 1): no per-byte chain walk. A literal c is the
+  // one byte at kLit + c, so literals and strings take one path. The table lives on the stack (a
+  // thread_local one in a -fPIC library costs a __tls_get_addr call per access).
+  static const struct LitBytes {
+    uint8_t b[256 + 16];
+    LitBytes() {
+      for (int c = 0; c < 256; c++) b[c] = (uint8_t)c;
+      for (int c = 256; c < 256 + 16; c++) b[c] = 0;  // the 16-byte copy's slack
+    }
+  } kLit;
+  const uint8_t* src[4096];
   uint16_t len[4096];
-  int nbits = 9, free_ent = kFirst;
+  for (int c = 0; c < 256; c++) {
+    src[c] = kLit.b + c;
+    len[c] = 1;
+  }
+  int nbits = 9, free_ent = kFirst, grow_at = (1 << 9) - 1;
   uint32_t mask = (1u << 9) - 1u;
   int64_t n_out = 0;
   int64_t bitpos = 0;
   const int64_t nbits_in = n_in * 8;
   const int64_t fast_end = (n_in - 4) * 8;  // a 32-bit load at bitpos >> 3 stays inside `in`
+  uint8_t* const out_end = out + cap;
   // the next code (MSB first): one unaligned big-endian 32-bit load while 4 bytes remain, else a
   // byte at a time; -1 when the input cannot fill a whole code (the strip's end)
   auto get = [&]() -> int {
-    if (bitpos <= fast_end) {
+    if (__builtin_expect(bitpos <= fast_end, 1)) {
       uint32_t w;
       memcpy(&w, in + (bitpos >> 3), 4);
       w = __builtin_bswap32(w);
@@ -85,20 +97,20 @@ int64_t lt_lzw_decode(const uint8_t* in, int64_t n_in, uint8_t* out, int64_t cap
       acc = (acc << 1) | ((in[bitpos >> 3] >> (7 - (bitpos & 7))) & 1u);
     return (int)acc;
   };
-  uint32_t old_pos = 0;  // the previous code's emission
-  int old_len = 0;
-  // copy L bytes from out[src] (src + L <= dst: earlier output, no overlap) to out[dst]
-  auto copy = [&](uint8_t* dst, const uint8_t* src, int L) {
-    if (L <= 16 && dst + 16 <= out + cap) {  // two unaligned 8-byte moves (the slack is output
-      uint64_t a, b;                          // space later codes overwrite)
-      memcpy(&a, src, 8);
-      memcpy(&b, src + 8, 8);
-      memcpy(dst, &a, 8);
-      if (L > 8) memcpy(dst + 8, &b, 8);
+  // copy L bytes from s (earlier output or kLit, no overlap with what is written) to d
+  auto copy = [&](uint8_t* d, const uint8_t* s, int L) {
+    if (__builtin_expect(L <= 16 && d + 16 <= out_end, 1)) {  // two unaligned 8-byte moves
+      uint64_t a, b;                                          // (the slack is output space
+      memcpy(&a, s, 8);                                       // later codes overwrite)
+      memcpy(&b, s + 8, 8);
+      memcpy(d, &a, 8);
+      if (L > 8) memcpy(d + 8, &b, 8);
     } else {
-      for (int k = 0; k < L; k++) dst[k] = src[k];
+      for (int k = 0; k < L; k++) d[k] = s[k];
     }
   };
+  uint32_t old_pos = 0;  // the previous code's emission
+  int old_len = 0;
   bool have_old = false;
   for (;;) {
     int code = get();
@@ -106,6 +118,7 @@ int64_t lt_lzw_decode(const uint8_t* in, int64_t n_in, uint8_t* out, int64_t cap
     if (code == kClear) {
       nbits = 9;
       mask = (1u << 9) - 1u;
+      grow_at = (1 << 9) - 1;
       free_ent = kFirst;
       code = get();
       if (code < 0 || code == kEoi) break;
@@ -117,7 +130,7 @@ int64_t lt_lzw_decode(const uint8_t* in, int64_t n_in, uint8_t* out, int64_t cap
       have_old = true;
       continue;
     }
-    if (!have_old) {  // data must start with a Clear code or a literal
+    if (__builtin_expect(!have_old, 0)) {  // data must start with a Clear code or a literal
       if (code >= 256) return LT_IO_ERR_DATA;
       if (n_out >= cap) return LT_IO_ERR_SPACE;
       out[n_out] = (uint8_t)code;
@@ -126,22 +139,12 @@ int64_t lt_lzw_decode(const uint8_t* in, int64_t n_in, uint8_t* out, int64_t cap
       have_old = true;
       continue;
     }
-    if (code < 256) {  // a literal
-      if (n_out >= cap) return LT_IO_ERR_SPACE;
-      out[n_out] = (uint8_t)code;
-      if (free_ent < 4096) {  // previous string + this byte: contiguous in out
-        pos[free_ent] = old_pos;
-        len[free_ent] = (uint16_t)(old_len + 1);
-        free_ent++;
-      }
-      old_pos = (uint32_t)n_out++;
-      old_len = 1;
-    } else if (code < free_ent) {
+    if (code < free_ent) {  // a literal or a table string
       const int L = len[code];
       if (n_out + L > cap) return LT_IO_ERR_SPACE;
-      copy(out + n_out, out + pos[code], L);
-      if (free_ent < 4096) {
-        pos[free_ent] = old_pos;
+      copy(out + n_out, src[code], L);
+      if (free_ent < 4096) {  // previous string + this one's first byte: contiguous in out
+        src[free_ent] = out + old_pos;
         len[free_ent] = (uint16_t)(old_len + 1);
         free_ent++;
       }
@@ -152,11 +155,11 @@ int64_t lt_lzw_decode(const uint8_t* in, int64_t n_in, uint8_t* out, int64_t cap
       // KwKwK: the previous string + its own first byte
       const int L = old_len + 1;
       if (n_out + L > cap) return LT_IO_ERR_SPACE;
-      uint8_t* dst = out + n_out;
-      const uint8_t* src = out + old_pos;
-      copy(dst, src, old_len);
-      dst[old_len] = src[0];
-      pos[free_ent] = (uint32_t)n_out;
+      uint8_t* d = out + n_out;
+      const uint8_t* s = out + old_pos;
+      copy(d, s, old_len);
+      d[old_len] = s[0];
+      src[free_ent] = d;
       len[free_ent] = (uint16_t)L;
       free_ent++;
       old_pos = (uint32_t)n_out;
@@ -165,9 +168,10 @@ int64_t lt_lzw_decode(const uint8_t* in, int64_t n_in, uint8_t* out, int64_t cap
     } else {
       return LT_IO_ERR_DATA;
     }
-    if (free_ent >= (1 << nbits) - 1 && nbits < kMaxBits) {
+    if (free_ent >= grow_at && nbits < kMaxBits) {
       nbits++;
       mask = (1u << nbits) - 1u;
+      grow_at = (1 << nbits) - 1;
     }
   }
   return n_out;
