@@ -224,13 +224,21 @@ class Engine:
 
     # --- load stage: index_eqn (rast_algebra, utils.py:447-484) ---
     def compile_index(self, program):
-        """hiprtc-compile an index_eqn.IndexProgram for this device (cached per program)."""
-        fn = ctypes.c_void_p()
-        prog = program.to_c()
-        with torch.cuda.device(self.device):
-            self._check(self.lib.lt_index_compile(self.ctx, ctypes.byref(prog), ctypes.byref(fn)),
-                        'lt_index_compile')
-        return IndexFn(fn, program, linear_form(program))
+        """hiprtc-compile an index_eqn.IndexProgram for this device (cached per program). A
+        program with an integer linear form is evaluated inside the analyze kernels, so its load
+        kernel is compiled only when something asks for an index raster (IndexFn.handle): a
+        job's analysis did not need the ~0.1 s."""
+        def build():
+            fn = ctypes.c_void_p()
+            prog = program.to_c()
+            with torch.cuda.device(self.device):
+                self._check(self.lib.lt_index_compile(self.ctx, ctypes.byref(prog),
+                                                      ctypes.byref(fn)), 'lt_index_compile')
+            return fn
+        lin = linear_form(program)
+        if lin is not None:
+            return IndexFn(None, program, lin, build=build)
+        return IndexFn(build(), program, lin)
 
     def index_tile(self, fn, bands, out=None, stream=None):
         """bands: [K, NB, P] band planes (NB = the program's band slots; unit pixel stride, or
@@ -353,10 +361,17 @@ class IndexFn:
     each winner from the band planes itself (analyze_tile(..., lin=fn.lin)), and the load kernel
     is needed only to materialise an index raster."""
 
-    def __init__(self, handle, program, lin=None):
-        self.handle = handle
+    def __init__(self, handle, program, lin=None, build=None):
+        self._handle = handle
+        self._build = build  # makes the handle on first use (Engine.compile_index)
         self.program = program
         self.lin = lin
+
+    @property
+    def handle(self):
+        if self._handle is None and self._build is not None:
+            self._handle, self._build = self._build(), None
+        return self._handle
 
 
 def linear_form(program):

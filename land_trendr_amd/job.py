@@ -228,7 +228,7 @@ class LocalJob:
         writer's label planes (device), None on the other ranks."""
         import torch
         from .distributed import TrendlineStream
-        from .engine import LABELS, TRENDLINE, get_engine, pack_valid_bits
+        from .engine import _DTYPE, LABELS, TRENDLINE, get_engine, pack_valid_bits
         from .index_eqn import IndexProgram
         from .runner import MosaicRunner, TileInput
         from .scene import build_scene, parse_date
@@ -342,7 +342,10 @@ class LocalJob:
                 dst[a:a + step] = src[a:a + step]
             list(pool.map(piece, range(0, n, step)))
 
-        tls = TrendlineStream(m.tile * 8, dev, depth=16, sink=sink) if cuda else None
+        # the ring's rows sized for the widest plane streamed (the labels-only job's winner rows
+        # are 4 bytes a pixel: half the pinned memory to allocate)
+        row_b = max(torch.empty(0, dtype=_DTYPE[f]).element_size() for f in tl_fields)
+        tls = TrendlineStream(m.tile * row_b, dev, depth=16, sink=sink) if cuda else None
         copied = {}  # tile -> event after its rows' D2H copies
 
         def push(k):

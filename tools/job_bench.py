@@ -152,6 +152,8 @@ def main():
     ap.add_argument('--diag', action='store_true',
                     help='after the job: one raster opened / decoded on 1 and all threads, and a '
                          'cProfile of output() run again (stderr)')
+    ap.add_argument('--profile', default=None, choices=('setup', 'parse', 'analyze', 'output'),
+                    help='run this step under cProfile (top entries by own time to stderr)')
     a = ap.parse_args()
     import torch
     from land_trendr_amd.ingest import host_threads
@@ -169,7 +171,20 @@ def main():
         files = None
         for step in ('setup', 'parse', 'analyze', 'output'):
             t0 = time.time()
-            res = getattr(j, step)()
+            if step == a.profile:  # this step under cProfile (top entries to stderr)
+                import cProfile
+                import io
+                import pstats
+                pr = cProfile.Profile()
+                pr.enable()
+                res = getattr(j, step)()
+                torch.cuda.synchronize()
+                pr.disable()
+                buf = io.StringIO()
+                pstats.Stats(pr, stream=buf).sort_stats('tottime').print_stats(25)
+                print(buf.getvalue(), file=sys.stderr, flush=True)
+            else:
+                res = getattr(j, step)()
             torch.cuda.synchronize()
             t[step] = time.time() - t0
             if step == 'output':
