@@ -293,7 +293,7 @@ class _Offsets:
 
 
 def ingest_stack(rast_fns, grid, mask_fns=None, bands=None, threads=None, pixels=None,
-                 raster_grid=None):
+                 raster_grid=None, on_raster=None):
     """parse_mapper over every analysis raster, as planes for analysis_reducer_batch.
 
     rast_fns: the (decompressed) analysis rasters, in the mapper order that becomes each pixel's
@@ -309,7 +309,9 @@ def ingest_stack(rast_fns, grid, mask_fns=None, bands=None, threads=None, pixels
     band_numbers=[nb], valid=[K, Q] uint8, n_pix=P, ranges=[(p0, p1, q0)]) with Q the points
     gathered; grid point p of range (p0, p1, q0) is column q0 + p - p0 (stack_range).
     raster_grid: (geotransform, rows, cols) when grid point p is pixel p of such a raster (the
-    job's raster order): rasters of that georeferencing are read by slicing, not by offsets."""
+    job's raster order): rasters of that georeferencing are read by slicing, not by offsets.
+    on_raster(k, bands_k [nb, Q], valid_k [Q]): called on the worker thread once raster k's planes
+    are complete (the job copies them to the GPU while the other rasters decode)."""
     from concurrent.futures import ThreadPoolExecutor
     lng, lat = grid if isinstance(grid, tuple) else grid_points(grid)
     P = len(lng)
@@ -384,6 +386,8 @@ def ingest_stack(rast_fns, grid, mask_fns=None, bands=None, threads=None, pixels
             take(m, midx, mok, mident, mval)
             drop = (mval == 0) if mok is None else (mok & (mval == 0))
             v &= ~drop
+        if on_raster is not None:
+            on_raster(k, out_bands[k], valid[k])
         return filename2date(fn)
 
     total = threads or host_threads()

@@ -212,10 +212,48 @@ class LocalJob:
         P = len(self.grid_xy[0])
         self.mosaic = Mosaic([P], self.tile_pixels, world, rank, 'round_robin')
         eqn_bands = sorted(parse_eqn_bands(self.settings['index_eqn']))
+        # on a GPU (LT_JOB_UPLOAD=whole), each raster's planes cross to the device as soon as they
+        # are decoded, on the worker that decoded them, while the other rasters decode: analyze()
+        # then starts from the device stack
+        self._dev_stack = None
+        up = self._stack_uploader(len(self.rast_fns), len(eqn_bands),
+                                  sum(t.n for t in self.mosaic.mine))
         self.stack = ingest_stack(self.rast_fns, self.grid_xy, self.mask_fns, bands=eqn_bands,
                                   pixels=[(t.p0, t.p1) for t in self.mosaic.mine],
-                                  raster_grid=self.raster_grid)
+                                  raster_grid=self.raster_grid, on_raster=up)
+        if up is not None and up.bands is not None:
+            import torch
+            torch.cuda.synchronize(up.device)
+            self._dev_stack = (up.bands, up.valid)
         return self.stack
+
+    def _stack_uploader(self, K, nb, Q):
+        """The per-raster H2D of parse() (None when the job does not run on a GPU, or
+        LT_JOB_UPLOAD is not 'whole')."""
+        import threading
+        import torch
+        if os.environ.get('LT_JOB_UPLOAD', 'whole') != 'whole' or not torch.cuda.is_available():
+            return None
+        if self.engine is not None and torch.device(self.engine.device).type != 'cuda':
+            return None
+        dev = torch.device('cuda', self.device if self.device is not None
+                           else torch.cuda.current_device())
+
+        class Up:
+            def __init__(self):
+                self.device, self.bands, self.valid = dev, None, None
+                self.lock = threading.Lock()
+
+            def __call__(self, k, b, v):
+                with self.lock:  # the device stack made by the first raster (its sample type)
+                    if self.bands is None:
+                        self.bands = torch.empty((K, nb, Q), dtype=torch.from_numpy(b[:0]).dtype,
+                                                 device=dev)
+                        self.valid = torch.empty((K, Q), dtype=torch.uint8, device=dev)
+                with torch.cuda.device(dev):
+                    self.bands[k].copy_(torch.from_numpy(b))
+                    self.valid[k].copy_(torch.from_numpy(v))
+        return Up()
 
     # 3. analysis_reducer, batched over pixel tiles: the mosaic path (runner.py) bench.py runs
     def analyze(self):
@@ -266,10 +304,15 @@ class LocalJob:
                  st['bands'].flags.c_contiguous and st['valid'].flags.c_contiguous and
                  st['bands'].nbytes + st['valid'].nbytes <= (64 << 30))
         if whole:
-            w_bands = torch.from_numpy(st['bands']).to(dev)
+            ds = getattr(self, '_dev_stack', None)
+            if ds is not None and ds[0].device == dev and ds[0].shape == st['bands'].shape:
+                w_bands, w_valid = ds  # uploaded raster by raster during parse()
+            else:
+                w_bands = torch.from_numpy(st['bands']).to(dev)
+                w_valid = torch.from_numpy(st['valid']).to(dev)
+            self._dev_stack = None
             if slots != list(range(st['bands'].shape[1])):
                 w_bands = w_bands[:, slots]
-            w_valid = torch.from_numpy(st['valid']).to(dev)
         items = []
         for t in m.mine:
             if whole:
