@@ -24,17 +24,24 @@ constexpr int kClear = 256, kEoi = 257, kFirst = 258, kMaxBits = 12;
 struct BitWriter {
   uint8_t* out;
   int64_t cap, n = 0;
-  uint32_t acc = 0;
+  uint64_t acc = 0;  // the pending bits, the oldest most significant (codes <= 12 bits)
   int nacc = 0;
   bool overflow = false;
   void put(int code, int nbits) {
     acc = (acc << nbits) | (uint32_t)code;
     nacc += nbits;
-    while (nacc >= 8) {
-      nacc -= 8;
-      byte((uint8_t)(acc >> nacc));
+    if (nacc >= 32) {  // four bytes at a time (MSB first)
+      nacc -= 32;
+      const uint32_t w = (uint32_t)(acc >> nacc);
+      if (__builtin_expect(n + 4 <= cap, 1)) {
+        const uint32_t be = __builtin_bswap32(w);
+        memcpy(out + n, &be, 4);
+        n += 4;
+      } else {
+        for (int k = 3; k >= 0; k--) byte((uint8_t)(w >> (8 * k)));
+      }
+      acc &= (1ull << nacc) - 1ull;
     }
-    acc &= (1u << nacc) - 1u;
   }
   void byte(uint8_t b) {
     if (n < cap) out[n] = b;
@@ -42,6 +49,10 @@ struct BitWriter {
     n++;
   }
   void flush() {
+    while (nacc >= 8) {
+      nacc -= 8;
+      byte((uint8_t)(acc >> nacc));
+    }
     if (nacc > 0) byte((uint8_t)(acc << (8 - nacc)));
     nacc = 0;
     acc = 0;
